@@ -1,0 +1,151 @@
+/*
+ * rtg.h — C-ABI of the MI355X wavefront path tracer (librtg.so).
+ *
+ * This is the drop-in boundary for RTBase's per-pixel render loop. It replaces, one for one:
+ *
+ *   RayTracer::render()                 RTBase/Renderer.h:876-885  -> rtg_render()
+ *     pathTracerTileBased/getTileID     RTBase/Renderer.h:820-853  (tile selection: tile_ids)
+ *     renderTile                        RTBase/Renderer.h:795-818  (pixel centre rays, splat)
+ *     pathTrace / computeDirect         RTBase/Renderer.h:328-392, 423-473
+ *     Scene::traverse / Scene::visible  RTBase/Scene.h:107-130, 161-169
+ *   Film::film / Film::SPP              RTBase/Imaging.h:201-261   -> rtg_film_*()
+ *   Film::clear                         RTBase/Imaging.h:252-256   -> rtg_clear()
+ *   Sampler::next (per-thread MTRandom) RTBase/Sampling.h:7-26     -> counter-based PCG32 stream
+ *                                       keyed by (seed, pixel, sample)
+ *
+ * Everything above the boundary (scene.json/.gem loading, texture decode, BVH build with its
+ * triangle permutation, light list, camera matrices, HDR writing) stays in the host; the host
+ * hands over the *flattened reference Scene* below. No C++ or torch types cross this ABI.
+ *
+ * Conventions: 0 = success, negative = error (rtg_last_error() gives a message, thread-local).
+ * A handle owns one GPU's copy of the scene and film; it is not thread-safe (one host thread
+ * per handle). Inputs are copied during rtg_create; the caller may free them afterwards.
+ */
+#ifndef RTG_H
+#define RTG_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTG_ABI_VERSION 1
+
+/* error codes */
+#define RTG_OK              0
+#define RTG_ERR_ARG        -1
+#define RTG_ERR_HIP        -2
+#define RTG_ERR_NO_DEVICE  -3
+#define RTG_ERR_NO_LIGHTS  -4
+#define RTG_ERR_ALLOC      -5
+
+/* Effective material kinds: RTBase has 8 BSDF classes but only three distinct
+ * behaviours plus a pdf quirk. */
+#define RTG_MAT_DIFFUSE   0  /* DiffuseBSDF             Materials.h:118-156 (pdf = z>=0 ? z/pi : 0)   */
+#define RTG_MAT_LAMBERT   1  /* Conductor/Dielectric/OrenNayar/Plastic stubs (pdf = z/pi, no clamp)  */
+#define RTG_MAT_MIRROR    2  /* MirrorBSDF              Materials.h:158-201                          */
+#define RTG_MAT_GLASS     3  /* GlassBSDF               Materials.h:252-318 (one-sided)              */
+
+typedef struct rtg_camera {        /* Camera, RTBase/Scene.h:10-70 */
+    float inv_proj[16];            /* inverseProjectionMatrix.m (row-major)   */
+    float camera[16];              /* camera.m (view -> world)                */
+    float origin[3];               /* origin = camera.mulPoint(0,0,0)         */
+    float width, height;           /* film size as the reference floats       */
+} rtg_camera;
+
+typedef struct rtg_material {      /* BSDF* + emission, RTBase/Materials.h:94-116 */
+    int32_t kind;                  /* RTG_MAT_*                                    */
+    int32_t two_sided;             /* BSDF::isTwoSided()                           */
+    int32_t texture;               /* albedo Texture* as an index into textures    */
+    float int_ior, ext_ior;        /* GlassBSDF::intIOR / extIOR (ignored otherwise) */
+    float emission[3];             /* BSDF::emission (isLight iff Lum > 0)         */
+} rtg_material;
+
+typedef struct rtg_texture {       /* Texture, RTBase/Imaging.h:16-130 */
+    int32_t width, height;
+    const float* texels;           /* width*height*3, Colour r,g,b row-major */
+} rtg_texture;
+
+typedef struct rtg_scene_desc {    /* Scene after Scene::build(), RTBase/Scene.h:72-106 */
+    uint32_t n_tris;               /* triangles in post-BVH-build order (Geometry.h:351 sort)  */
+    const float* positions;        /* n_tris*9: vertices[0..2].p                               */
+    const float* normals;          /* n_tris*9: vertices[0..2].normal                          */
+    const float* uvs;              /* n_tris*6: (u,v) of vertices[0..2]                        */
+    const uint32_t* material;      /* n_tris: Triangle::materialIndex                          */
+    uint32_t n_nodes;              /* BVHNode tree flattened in DFS pre-order, root = 0        */
+    const float* node_bounds;      /* n_nodes*6: bounds.min.xyz, bounds.max.xyz                */
+    const int32_t* node_links;     /* n_nodes*4: l, r (-1 = none), startIndex, endIndex        */
+    uint32_t n_materials;
+    const rtg_material* materials;
+    uint32_t n_textures;
+    const rtg_texture* textures;
+    int32_t env_texture;           /* -1: BackgroundColour(0,0,0); else EnvironmentMap(tex)    */
+    uint32_t n_lights;             /* Scene::lights in order                                   */
+    const int32_t* lights;         /* -1 = the environment light, else a triangle index        */
+    rtg_camera camera;
+} rtg_scene_desc;
+
+typedef struct rtg_stats {
+    uint64_t paths;                /* camera paths traced                                      */
+    uint64_t extension_rays;       /* closest-hit queries (Scene::traverse)                    */
+    uint64_t shadow_rays;          /* any-hit queries (Scene::visible)                         */
+    uint64_t node_visits;          /* counting builds only (0 otherwise)                       */
+    uint64_t tri_tests;            /* counting builds only (0 otherwise)                       */
+    double   render_ms;            /* device time of the last rtg_render call                  */
+    double   extend_ms;            /* device time spent in closest-hit kernels (last call)     */
+    double   shadow_ms;            /* device time spent in any-hit kernels (last call)         */
+    double   shade_ms;             /* device time spent in generate/shade/accumulate kernels   */
+} rtg_stats;
+
+typedef struct rtg_handle rtg_handle;
+
+int32_t     rtg_abi_version(void);
+const char* rtg_last_error(void);
+int         rtg_device_count(int* count);
+
+/* Upload the scene to device `device` (HBM); allocates the film (width*height RGB float). */
+int  rtg_create(int device, const rtg_scene_desc* desc, rtg_handle** out);
+void rtg_destroy(rtg_handle* h);
+
+/* Tracing options. max_depth is RTBase's MAX_DEPTH (Renderer.h:20, default 4): a path has at
+ * most max_depth+2 closest-hit segments. flags: RTG_OPT_CULL enables the conservative distance
+ * culling (without it traversal visits exactly the reference's node set: verification mode);
+ * RTG_OPT_COUNT runs the counting kernels (node / triangle tests in rtg_stats);
+ * RTG_OPT_TIMING records HIP events around every launch (per-kernel-class ms in rtg_stats).
+ * max_paths_in_flight bounds the paths of one wavefront chunk (0 = keep, default 4M). */
+#define RTG_OPT_CULL   1
+#define RTG_OPT_COUNT  2
+#define RTG_OPT_TIMING 4
+int  rtg_set_options(rtg_handle* h, int max_depth, int flags, uint32_t max_paths_in_flight);
+
+/* Add samples [first_sample, first_sample+n_samples) of every pixel in the listed 32x32 tiles
+ * (tile id = ty*tilesX + tx, RTBase TILE_SIZE=32; tile_ids=NULL = all tiles) to the film, in
+ * sample order per pixel. Equivalent to n_samples calls of RayTracer::render() with the
+ * deterministic sampler. Synchronous unless rtg_render_async is used. */
+int  rtg_render(rtg_handle* h, uint32_t first_sample, uint32_t n_samples, uint64_t seed,
+                const uint32_t* tile_ids, uint32_t n_tiles);
+int  rtg_render_async(rtg_handle* h, uint32_t first_sample, uint32_t n_samples, uint64_t seed,
+                      const uint32_t* tile_ids, uint32_t n_tiles, void* hip_stream);
+int  rtg_synchronize(rtg_handle* h);
+
+/* Film access: the unnormalised sum (Film::film) and the sample count (Film::SPP). */
+int  rtg_film_read(rtg_handle* h, float* rgb_sum /* width*height*3 */, uint32_t* spp);
+int  rtg_film_copy_device(rtg_handle* h, void* dst_device /* width*height*3 floats */);
+int  rtg_film_load(rtg_handle* h, const float* rgb_sum, uint32_t spp);  /* resume */
+int  rtg_clear(rtg_handle* h);
+int  rtg_get_stats(rtg_handle* h, rtg_stats* out);
+
+/* Low-level ray queries on the uploaded scene (test / oracle comparison surface).
+ * rays: n*8 floats (o.xyz, tmax, dir.xyz, pad). For closest-hit, tmax is ignored and the result
+ * is n*4 (t, id-as-float-bits, alpha, beta) with t = FLT_MAX on miss (IntersectionData,
+ * Geometry.h:231-238). For any-hit, tmax is Scene::visible's maxT and the result is n int32
+ * (1 = visible). Device-side arrays are allocated internally; inputs are host pointers. */
+int  rtg_trace_closest(rtg_handle* h, const float* rays, uint32_t n, float* hits);
+int  rtg_trace_visible(rtg_handle* h, const float* rays, uint32_t n, int32_t* visible);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTG_H */

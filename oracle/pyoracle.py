@@ -1,0 +1,95 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes access to the C oracle (oracle/rt_oracle.c).
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg; the
+product package (raytracingrenderer_amd) never imports it.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+
+_libs = {}
+
+
+def lib(flavour="rtm"):
+    """flavour 'rtm': shared bit-reproducible math (GPU parity); 'libm': the C library's math."""
+    if flavour not in _libs:
+        L = C.CDLL(os.path.join(BUILD, "liboracle_%s.so" % flavour))
+        vp, f32p, u32p, i32p = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.POINTER(C.c_int32)
+        L.or_create.restype = vp
+        L.or_create.argtypes = [vp, C.c_int]
+        L.or_destroy.argtypes = [vp]
+        L.or_set_max_depth.argtypes = [vp, C.c_int]
+        L.or_render.restype = C.c_int
+        L.or_render.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32, C.c_int, f32p,
+                                C.POINTER(C.c_uint64), C.c_int]
+        L.or_trace_paths.argtypes = [vp, u32p, u32p, C.c_uint32, C.c_uint64, f32p]
+        L.or_trace_closest.argtypes = [vp, f32p, C.c_uint32, f32p]
+        L.or_trace_visible.argtypes = [vp, f32p, C.c_uint32, i32p]
+        L.or_camera_rays.argtypes = [vp, u32p, C.c_uint32, f32p]
+        for fn in ("or_acosf", "or_sinf", "or_cosf"):
+            getattr(L, fn).restype = C.c_float
+            getattr(L, fn).argtypes = [C.c_float]
+        L.or_atan2f.restype = C.c_float
+        L.or_atan2f.argtypes = [C.c_float, C.c_float]
+        _libs[flavour] = L
+    return _libs[flavour]
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class Oracle:
+    def __init__(self, scene, max_depth=4, flavour="rtm"):
+        self.L = lib(flavour)
+        self.scene = scene  # keeps the desc alive
+        self.h = self.L.or_create(C.cast(scene.desc_ptr, C.c_void_p), max_depth)
+        if not self.h:
+            raise RuntimeError("or_create failed")
+        self.W, self.H = scene.width, scene.height
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.or_destroy(self.h)
+            self.h = None
+
+    def render(self, n_samples, first=0, seed=1234, tiles=None, threads=1, film=None, count=False):
+        if film is None:
+            film = np.zeros((self.H, self.W, 3), np.float32)
+        t = None if tiles is None else np.ascontiguousarray(tiles, np.uint32)
+        counts = np.zeros(5, np.uint64)
+        rc = self.L.or_render(self.h, first, n_samples, seed, _p(t, C.c_uint32) if t is not None else None,
+                              0 if t is None else len(t), threads, _p(film, C.c_float),
+                              _p(counts, C.c_uint64), 1 if count else 0)
+        if rc != 0:
+            raise RuntimeError("or_render failed")
+        return film, counts
+
+    def trace_paths(self, pixels, samples, seed=1234):
+        p = np.ascontiguousarray(pixels, np.uint32)
+        s = np.ascontiguousarray(samples, np.uint32)
+        out = np.zeros((len(p), 3), np.float32)
+        self.L.or_trace_paths(self.h, _p(p, C.c_uint32), _p(s, C.c_uint32), len(p), seed, _p(out, C.c_float))
+        return out
+
+    def trace_closest(self, rays):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        out = np.zeros((len(r), 4), np.float32)
+        self.L.or_trace_closest(self.h, _p(r, C.c_float), len(r), _p(out, C.c_float))
+        return out
+
+    def trace_visible(self, rays):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        out = np.zeros(len(r), np.int32)
+        self.L.or_trace_visible(self.h, _p(r, C.c_float), len(r), _p(out, C.c_int32))
+        return out
+
+    def camera_rays(self, pixels):
+        p = np.ascontiguousarray(pixels, np.uint32)
+        out = np.zeros((len(p), 6), np.float32)
+        self.L.or_camera_rays(self.h, _p(p, C.c_uint32), len(p), _p(out, C.c_float))
+        return out

@@ -1,0 +1,675 @@
+/*
+ * rt_oracle.c — TEST INFRASTRUCTURE ONLY. CPU restatement of RTBase's render loop, used as the
+ * parity checker (tests/, __graft_entry__.smoke()) and as the CPU baseline leg of bench.py.
+ * The product (librtg.so / librth.so) never links or calls this file.
+ *
+ * It restates, function for function and in the reference's floating-point operation order:
+ *   RayTracer::render / pathTracerTileBased / getTileID / renderTile  RTBase/Renderer.h:795-885
+ *   RayTracer::pathTrace                                             RTBase/Renderer.h:328-392
+ *   RayTracer::computeDirect                                         RTBase/Renderer.h:423-473
+ *   Scene::traverse / visible / sampleLight / calculateShadingData   RTBase/Scene.h:107-203
+ *   BVHNode::traverse / traverseVisible (left-first DFS, no culling) RTBase/Geometry.h:399-462
+ *   AABB::rayAABB, Triangle::init / rayIntersect / sample / gNormal  RTBase/Geometry.h:72-184
+ *   Camera::generateRay                                              RTBase/Scene.h:43-54
+ *   Diffuse/Mirror/Glass BSDF + the Lambert stubs                    RTBase/Materials.h:118-465
+ *   AreaLight / EnvironmentMap sample + evaluate                     RTBase/Lights.h:30-201
+ *   Texture::sample                                                  RTBase/Imaging.h:72-94
+ *   SamplingDistributions, SphericalCoordinates, Frame               RTBase/Sampling.h, Core.h
+ * on the flattened Scene of include/rtg.h (the host front-end's output), with the deterministic
+ * PCG32 sampler of SURVEY.md Appendix B injected in place of MTRandom (Sampling.h:13-26).
+ *
+ * Argument-evaluation order: the reference writes cosineSampleHemisphere(sampler.next(),
+ * sampler.next()) (Materials.h:129) and uniformSampleSphere(sampler.next(), sampler.next())
+ * (Lights.h:145); g++ evaluates those arguments right to left, so the FIRST draw becomes r2.
+ *
+ * Transcendentals: built twice. ORACLE_LIBM=1 calls the C library's acosf/sinf/cosf/atan2f
+ * (what the reference gets on Linux); otherwise the shared bit-reproducible rtm_* functions of
+ * include/rtg_math.h (what the GPU build uses), so GPU-vs-oracle can be compared bit for bit.
+ * Compile with -ffp-contract=off.
+ */
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/rtg.h"
+#include "../include/rtg_math.h"
+
+#if ORACLE_LIBM
+#define O_ACOSF acosf
+#define O_SINF sinf
+#define O_COSF cosf
+#define O_ATAN2F atan2f
+#else
+#define O_ACOSF rtm_acosf
+#define O_SINF rtm_sinf
+#define O_COSF rtm_cosf
+#define O_ATAN2F rtm_atan2f
+#endif
+
+#define O_EPS 1e-4f
+#define O_PI 3.14159265358979323846 /* M_PI */
+
+typedef struct { float x, y, z; } V3;
+typedef struct { float r, g, b; } Col;
+
+static V3 v3(float x, float y, float z) { V3 v; v.x = x; v.y = y; v.z = z; return v; }
+static V3 vadd(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static V3 vsub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static V3 vmuls(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+static V3 vmulv(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+static float vdot(V3 a, V3 b) { return ((a.x * b.x) + (a.y * b.y)) + (a.z * b.z); }
+static V3 vcross(V3 a, V3 b) { return v3((a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x)); }
+static float vlen2(V3 a) { return ((a.x * a.x) + (a.y * a.y)) + (a.z * a.z); }
+static float vlen(V3 a) { return sqrtf(((a.x * a.x) + (a.y * a.y)) + (a.z * a.z)); }
+static V3 vnorm(V3 a) { float l = 1.0f / sqrtf(((a.x * a.x) + (a.y * a.y)) + (a.z * a.z)); return v3(a.x * l, a.y * l, a.z * l); }
+static V3 Vmin(V3 a, V3 b) { return v3(a.x < b.x ? a.x : b.x, a.y < b.y ? a.y : b.y, a.z < b.z ? a.z : b.z); }
+static V3 Vmax(V3 a, V3 b) { return v3(a.x > b.x ? a.x : b.x, a.y > b.y ? a.y : b.y, a.z > b.z ? a.z : b.z); }
+static float std_max(float a, float b) { return (a < b) ? b : a; }
+static float std_min(float a, float b) { return (b < a) ? b : a; }
+static float win_max(float a, float b) { return a > b ? a : b; } /* windows.h macro */
+static float win_min(float a, float b) { return a < b ? a : b; }
+
+static Col col(float r, float g, float b) { Col c; c.r = r; c.g = g; c.b = b; return c; }
+static Col cadd(Col a, Col b) { return col(a.r + b.r, a.g + b.g, a.b + b.b); }
+static Col cmul(Col a, Col b) { return col(a.r * b.r, a.g * b.g, a.b * b.b); }
+static Col cmuls(Col a, float s) { return col(a.r * s, a.g * s, a.b * s); }
+static Col cdivs(Col a, float s) { return col(a.r / s, a.g / s, a.b / s); }
+static float clum(Col c) { return ((0.2126f * c.r) + (0.7152f * c.g)) + (0.0722f * c.b); }
+
+typedef struct { V3 u, v, w; } Frame;
+static Frame frame_from(V3 n) { /* Core.h:513-527 */
+    Frame f;
+    f.w = vnorm(n);
+    if (fabsf(f.w.x) > fabsf(f.w.y)) {
+        float l = 1.0f / sqrtf(f.w.x * f.w.x + f.w.z * f.w.z);
+        f.u = v3(f.w.z * l, 0.0f, -f.w.x * l);
+    } else {
+        float l = 1.0f / sqrtf(f.w.y * f.w.y + f.w.z * f.w.z);
+        f.u = v3(0, f.w.z * l, -f.w.y * l);
+    }
+    f.v = vcross(f.w, f.u);
+    return f;
+}
+static V3 to_local(const Frame* f, V3 a) { return v3(vdot(a, f->u), vdot(a, f->v), vdot(a, f->w)); }
+static V3 to_world(const Frame* f, V3 a) { return vadd(vadd(vmuls(f->u, a.x), vmuls(f->v, a.y)), vmuls(f->w, a.z)); }
+
+/* ------------------------------------------------------------------ sampler */
+typedef struct { uint64_t s, inc; } Pcg;
+static uint32_t pcg_u32(Pcg* p) {
+    uint64_t o = p->s;
+    p->s = o * 6364136223846793005ULL + p->inc;
+    uint32_t x = (uint32_t)(((o >> 18u) ^ o) >> 27u);
+    uint32_t r = (uint32_t)(o >> 59u);
+    return (x >> r) | (x << ((0u - r) & 31u));
+}
+static void pcg_init(Pcg* p, uint64_t seed, uint64_t seq) {
+    p->s = 0;
+    p->inc = (seq << 1u) | 1u;
+    pcg_u32(p);
+    p->s += seed;
+    pcg_u32(p);
+}
+static float pcg_next(Pcg* p) { return (float)(pcg_u32(p) >> 8) * (1.0f / 16777216.0f); }
+
+/* ------------------------------------------------------------------ scene */
+typedef struct {
+    V3 p[3], n[3];
+    float u[3], v[3];
+    V3 e1, e2, nrm;
+    float area, d;
+    uint32_t mat;
+} Tri;
+typedef struct { V3 mn, mx; int l, r, start, end; } Node;
+typedef struct { int w, h; const float* t; } Tex;
+
+struct or_scene {
+    int ntri, nnode, nlight, env_tex, max_depth;
+    Tri* tri;
+    Node* node;
+    rtg_material* mat;
+    Tex* tex;
+    float* texels;
+    int* light;
+    rtg_camera cam;
+    int W, H;
+};
+
+typedef struct {
+    uint64_t ext_rays, shadow_rays, nodes, tris;
+} Counts;
+
+typedef struct { V3 o, dir, inv; } Ray;
+static Ray ray_make(V3 o, V3 d) { Ray r; r.o = o; r.dir = d; r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); return r; }
+
+/* AABB::rayAABB (Geometry.h:173-184) */
+static int ray_aabb(const Node* b, const Ray* r) {
+    V3 tmin = vmulv(vsub(b->mn, r->o), r->inv);
+    V3 tmax = vmulv(vsub(b->mx, r->o), r->inv);
+    V3 ten = Vmin(tmin, tmax), tex = Vmax(tmin, tmax);
+    float te = std_max(std_max(ten.x, ten.y), ten.z);
+    float tx = std_min(std_min(tex.x, tex.y), tex.z);
+    if (tx < te || tx < 0) return 0;
+    return 1;
+}
+
+/* Triangle::rayIntersect (Geometry.h:89-105) */
+static int tri_hit(const Tri* T, const Ray* r, float* t, float* u, float* v) {
+    float denom = vdot(T->nrm, r->dir);
+    if (denom == 0) return 0;
+    *t = (T->d - vdot(T->nrm, r->o)) / denom;
+    if (*t < 0) return 0;
+    V3 p = vadd(r->o, vmuls(r->dir, *t));
+    float inv_area = 1.0f / vdot(vcross(T->e1, T->e2), T->nrm);
+    *u = vdot(vcross(T->e1, vsub(p, T->p[1])), T->nrm) * inv_area;
+    if (*u < 0 || *u > 1.0f) return 0;
+    *v = vdot(vcross(T->e2, vsub(p, T->p[2])), T->nrm) * inv_area;
+    if (*v < 0 || (*u + *v) > 1.0f) return 0;
+    return 1;
+}
+
+typedef struct { int id; float t, alpha, beta, gamma; } Isect;
+
+/* BVHNode::traverse (Geometry.h:399-427): recursive left-then-right, no ordering/culling */
+static void traverse(const struct or_scene* s, int ni, const Ray* r, Isect* is, Counts* c) {
+    const Node* n = &s->node[ni];
+    if (c) c->nodes++;
+    if (!ray_aabb(n, r)) return;
+    if (n->l < 0 && n->r < 0) {
+        for (int i = n->start; i < n->end; i++) {
+            float t, u, v;
+            if (c) c->tris++;
+            if (tri_hit(&s->tri[i], r, &t, &u, &v)) {
+                if (t < is->t && t > O_EPS) {
+                    is->t = t;
+                    is->id = i;
+                    is->alpha = u;
+                    is->beta = v;
+                    is->gamma = 1.0f - (u + v);
+                }
+            }
+        }
+        return;
+    }
+    if (n->l >= 0) traverse(s, n->l, r, is, c);
+    if (n->r >= 0) traverse(s, n->r, r, is, c);
+}
+
+/* BVHNode::traverseVisible (Geometry.h:435-462) */
+static int traverse_visible(const struct or_scene* s, int ni, const Ray* r, float maxT, Counts* c) {
+    const Node* n = &s->node[ni];
+    if (c) c->nodes++;
+    if (!ray_aabb(n, r)) return 1;
+    if (n->l < 0 && n->r < 0) {
+        for (int i = n->start; i < n->end; i++) {
+            float t, u, v;
+            if (c) c->tris++;
+            if (tri_hit(&s->tri[i], r, &t, &u, &v)) {
+                if (t >= maxT || t <= O_EPS) continue;
+                return 0;
+            }
+        }
+        return 1;
+    }
+    if (!traverse_visible(s, n->l, r, maxT, c)) return 0;
+    return traverse_visible(s, n->r, r, maxT, c);
+}
+
+static Isect scene_traverse(const struct or_scene* s, const Ray* r, Counts* c) {
+    Isect is;
+    is.id = -1;
+    is.t = FLT_MAX;
+    is.alpha = is.beta = is.gamma = 0;
+    if (c) c->ext_rays++;
+    traverse(s, 0, r, &is, c);
+    return is;
+}
+
+/* Scene::visible (Scene.h:161-169) */
+static int scene_visible(const struct or_scene* s, V3 p1, V3 p2, Counts* c) {
+    V3 dir = vsub(p2, p1);
+    float maxT = vlen(dir) - (2.0f * O_EPS);
+    dir = vnorm(dir);
+    Ray r = ray_make(vadd(p1, vmuls(dir, O_EPS)), dir);
+    if (c) c->shadow_rays++;
+    return traverse_visible(s, 0, &r, maxT, c);
+}
+
+/* Texture::sample (Imaging.h:72-94) */
+static Col tex_sample(const struct or_scene* s, int ti, float tu, float tv) {
+    const Tex* T = &s->tex[ti];
+    float u = std_max(0.0f, fabsf(tu)) * T->w;
+    float v = std_max(0.0f, fabsf(tv)) * T->h;
+    int x = (int)floorf(u), y = (int)floorf(v);
+    float fu = u - x, fv = v - y;
+    float w0 = (1.0f - fu) * (1.0f - fv), w1 = fu * (1.0f - fv), w2 = (1.0f - fu) * fv, w3 = fu * fv;
+    x = x % T->w;
+    y = y % T->h;
+    const float* a = T->t + (size_t)(y * T->w + x) * 3;
+    const float* b = T->t + (size_t)(y * T->w + ((x + 1) % T->w)) * 3;
+    const float* cc = T->t + (size_t)(((y + 1) % T->h) * T->w + x) * 3;
+    const float* d = T->t + (size_t)(((y + 1) % T->h) * T->w + ((x + 1) % T->w)) * 3;
+    Col s0 = col(a[0], a[1], a[2]), s1 = col(b[0], b[1], b[2]), s2 = col(cc[0], cc[1], cc[2]), s3 = col(d[0], d[1], d[2]);
+    return cadd(cadd(cadd(cmuls(s0, w0), cmuls(s1, w1)), cmuls(s2, w2)), cmuls(s3, w3));
+}
+
+/* SamplingDistributions (Sampling.h:44-69) + SphericalCoordinates (Core.h:547-550) */
+static V3 sph_to_world(float theta, float phi) {
+    return v3(O_COSF(phi) * O_SINF(theta), O_SINF(phi) * O_SINF(theta), O_COSF(theta));
+}
+static V3 cosine_sample_hemisphere(float r1, float r2) {
+    float theta = O_ACOSF(sqrtf(r1));
+    float phi = (float)(2.0f * O_PI * r2);
+    return sph_to_world(theta, phi);
+}
+static V3 uniform_sample_sphere(float r1, float r2) {
+    float theta = O_ACOSF(1 - 2 * r1);
+    float phi = (float)(2.0f * O_PI * r2);
+    return sph_to_world(theta, phi);
+}
+
+/* EnvironmentMap::evaluate (Lights.h:150-157) */
+static Col env_eval(const struct or_scene* s, V3 wi) {
+    float u = O_ATAN2F(wi.z, wi.x);
+    u = (float)((u < 0.0f) ? u + (2.0f * O_PI) : u);
+    u = (float)(u / (2.0f * O_PI));
+    float v = (float)(O_ACOSF(wi.y) / O_PI);
+    return tex_sample(s, s->env_tex, u, v);
+}
+
+/* fresnelDielectric (Materials.h:55-77) */
+static float fresnel_dielectric(float cos_i, float ior_int, float ior_ext, V3* wt, V3 wol) {
+    float ior = ior_int / ior_ext;
+    float sin_i = sqrtf(1 - (cos_i * cos_i));
+    float sin_t = ior * sin_i;
+    float ior2sin2 = (ior * ior) * (1 - (cos_i * cos_i));
+    if (ior2sin2 > 1.0f) return 1.0f;
+    float cos_t = sqrtf(1 - (sin_t * sin_t));
+    *wt = v3(-ior * wol.x, -ior * wol.y, -cos_t);
+    float fpa = (cos_i - ior * cos_t) / (cos_i + ior * cos_t);
+    float fpe = (ior * cos_i - cos_t) / (ior * cos_i + ior * cos_t);
+    float avg = ((fpa * fpa) + (fpe * fpe)) * 0.5f;
+    return std_max(0.0f, std_min(1.0f, avg));
+}
+
+typedef struct {
+    V3 x, wo, sN;
+    float tu, tv;
+    Frame frame;
+    const rtg_material* bsdf;
+    float t;
+} Shading;
+
+/* Scene::calculateShadingData (Scene.h:174-203) */
+static Shading shading_data(const struct or_scene* s, const Isect* is, const Ray* r) {
+    Shading sd;
+    memset(&sd, 0, sizeof(sd));
+    sd.t = is->t;
+    sd.wo = vneg(r->dir);
+    if (!(is->t < FLT_MAX)) return sd;
+    const Tri* T = &s->tri[is->id];
+    sd.x = vadd(r->o, vmuls(r->dir, is->t));
+    V3 n = vadd(vadd(vmuls(T->n[0], is->alpha), vmuls(T->n[1], is->beta)), vmuls(T->n[2], is->gamma));
+    sd.sN = vnorm(n);
+    sd.tu = (T->u[0] * is->alpha + T->u[1] * is->beta) + T->u[2] * is->gamma;
+    sd.tv = (T->v[0] * is->alpha + T->v[1] * is->beta) + T->v[2] * is->gamma;
+    sd.bsdf = &s->mat[T->mat];
+    if (sd.bsdf->two_sided && vdot(sd.wo, sd.sN) < 0) sd.sN = vneg(sd.sN);
+    sd.frame = frame_from(sd.sN);
+    return sd;
+}
+
+static int is_spec(const rtg_material* m) { return m->kind == RTG_MAT_MIRROR || m->kind == RTG_MAT_GLASS; }
+static int is_light(const rtg_material* m) { return clum(col(m->emission[0], m->emission[1], m->emission[2])) > 0; }
+
+/* BSDF::evaluate for the non-specular kinds (albedo / M_PI as float) */
+static Col bsdf_eval(const struct or_scene* s, const Shading* sd) {
+    return cdivs(tex_sample(s, sd->bsdf->texture, sd->tu, sd->tv), (float)O_PI);
+}
+
+/* RayTracer::computeDirect (Renderer.h:423-473) */
+static Col compute_direct(const struct or_scene* s, const Shading* sd, Pcg* smp, Counts* c) {
+    if (is_spec(sd->bsdf)) return col(0.0f, 0.0f, 0.0f);
+    float pmf = 1.f / (float)s->nlight;
+    int li = (int)((float)s->nlight * pcg_next(smp));
+    if (s->nlight - 1 < li) li = s->nlight - 1; /* (std::min)(a, b) */
+    int lt = s->light[li];
+    if (lt >= 0) { /* AreaLight::sample -> Triangle::sample (Geometry.h:114-126) */
+        const Tri* T = &s->tri[lt];
+        float r1 = pcg_next(smp);
+        float r2 = pcg_next(smp);
+        float alpha = 1 - sqrtf(r1);
+        float beta = r2 * sqrtf(r1);
+        float gamma = 1.0f - (alpha + beta);
+        float pdf = 1.0f / T->area;
+        V3 p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+        const float* e = s->mat[T->mat].emission;
+        Col emitted = col(e[0], e[1], e[2]);
+        V3 wi = vsub(p, sd->x);
+        float l = vlen2(wi);
+        wi = vnorm(wi);
+        V3 gn = vmuls(T->nrm, vdot(T->n[0], T->nrm) > 0 ? 1.0f : -1.0f); /* Triangle::gNormal */
+        float G = (win_max(vdot(wi, sd->sN), 0.0f) * win_max(-vdot(wi, gn), 0.0f)) / l;
+        if (G > 0) {
+            if (scene_visible(s, sd->x, p, c))
+                return cdivs(cmuls(cmul(bsdf_eval(s, sd), emitted), G), pmf * pdf);
+        }
+    } else { /* EnvironmentMap::sample */
+        float q2 = pcg_next(smp);
+        float q1 = pcg_next(smp);
+        V3 wi = uniform_sample_sphere(q1, q2);
+        float pdf = (float)(1.0f / (4.0f * O_PI));
+        Col emitted = env_eval(s, wi);
+        float G = win_max(vdot(wi, sd->sN), 0.0f);
+        if (G > 0) {
+            if (scene_visible(s, sd->x, vadd(sd->x, vmuls(wi, 10000.0f)), c))
+                return cdivs(cmuls(cmul(bsdf_eval(s, sd), emitted), G), pmf * pdf);
+        }
+    }
+    return col(0.0f, 0.0f, 0.0f);
+}
+
+/* BSDF::sample for the three effective behaviours */
+static V3 bsdf_sample(const struct or_scene* s, const Shading* sd, Pcg* smp, Col* refl, float* pdf) {
+    const rtg_material* m = sd->bsdf;
+    Col alb = tex_sample(s, m->texture, sd->tu, sd->tv);
+    if (m->kind == RTG_MAT_DIFFUSE || m->kind == RTG_MAT_LAMBERT) {
+        float q2 = pcg_next(smp); /* cosineSampleHemisphere(sampler.next(), sampler.next()) */
+        float q1 = pcg_next(smp);
+        V3 wl = cosine_sample_hemisphere(q1, q2);
+        if (m->kind == RTG_MAT_DIFFUSE) *pdf = (float)((wl.z >= 0.0f) ? (wl.z / O_PI) : 0.0f); /* cosineHemispherePDF */
+        else *pdf = (float)(wl.z / O_PI);                                                      /* Lambert stubs */
+        *refl = cdivs(alb, (float)O_PI);
+        return to_world(&sd->frame, wl);
+    }
+    if (m->kind == RTG_MAT_MIRROR) { /* Materials.h:167-177 */
+        V3 wol = to_local(&sd->frame, sd->wo);
+        *pdf = 1.0f;
+        *refl = alb;
+        return to_world(&sd->frame, v3(-wol.x, -wol.y, wol.z));
+    }
+    /* GlassBSDF::sample (Materials.h:265-294) */
+    V3 wol = to_local(&sd->frame, sd->wo);
+    float cos_i = fabsf(wol.z);
+    int enter = wol.z > 0.0f;
+    float eta_i = enter ? m->ext_ior : m->int_ior;
+    float eta_t = enter ? m->int_ior : m->ext_ior;
+    V3 wt = v3(0, 0, 0), wi;
+    float R = fresnel_dielectric(cos_i, eta_i, eta_t, &wt, wol);
+    if (!enter) wt.z = -wt.z;
+    int reflect = (R == 1.0f || pcg_next(smp) < R);
+    if (reflect) {
+        wi = v3(-wol.x, -wol.y, wol.z);
+        *pdf = R;
+        *refl = cmuls(alb, R);
+    } else {
+        wi = wt;
+        *pdf = 1.0f - R;
+        *refl = cmuls(alb, 1.0f - R);
+    }
+    return to_world(&sd->frame, wi);
+}
+
+/* RayTracer::pathTrace (Renderer.h:328-392) */
+static Col path_trace(const struct or_scene* s, Ray* r, Col* thr, int depth, Pcg* smp, int can_hit, Counts* c) {
+    Isect is = scene_traverse(s, r, c);
+    Shading sd = shading_data(s, &is, r);
+    if (sd.t < FLT_MAX) {
+        if (is_light(sd.bsdf)) {
+            if (can_hit) {
+                const float* e = sd.bsdf->emission;
+                return cmul(*thr, col(e[0], e[1], e[2]));
+            }
+            return col(0.0f, 0.0f, 0.0f);
+        }
+        Col direct = cmul(*thr, compute_direct(s, &sd, smp, c));
+        if (depth > s->max_depth) return direct;
+        float rrp = win_min(clum(*thr), 0.9f);
+        if (pcg_next(smp) < rrp) *thr = cdivs(*thr, rrp);
+        else return direct;
+        Col ind;
+        float pdf;
+        V3 wi = bsdf_sample(s, &sd, smp, &ind, &pdf);
+        if (is_spec(sd.bsdf)) *thr = cdivs(cmul(*thr, ind), pdf);
+        else *thr = cdivs(cmuls(cmul(*thr, ind), fabsf(vdot(wi, sd.sN))), pdf);
+        *r = ray_make(vadd(sd.x, vmuls(wi, O_EPS)), wi);
+        return cadd(direct, path_trace(s, r, thr, depth + 1, smp, is_spec(sd.bsdf), c));
+    }
+    if (s->env_tex < 0) return col(0.0f, 0.0f, 0.0f); /* BackgroundColour(0,0,0) */
+    return env_eval(s, r->dir);
+}
+
+/* Camera::generateRay (Scene.h:43-54) */
+static Ray camera_ray(const struct or_scene* s, float x, float y) {
+    const rtg_camera* c = &s->cam;
+    float xp = x / c->width;
+    float yp = 1.0f - (y / c->height);
+    xp = (xp * 2.0f) - 1.0f;
+    yp = (yp * 2.0f) - 1.0f;
+    const float* m = c->inv_proj;
+    V3 d = v3(((xp * m[0] + yp * m[1]) + 1.0f * m[2]) + m[3], ((xp * m[4] + yp * m[5]) + 1.0f * m[6]) + m[7],
+              ((xp * m[8] + yp * m[9]) + 1.0f * m[10]) + m[11]);
+    const float* k = c->camera;
+    d = v3((d.x * k[0] + d.y * k[1]) + d.z * k[2], (d.x * k[4] + d.y * k[5]) + d.z * k[6], (d.x * k[8] + d.y * k[9]) + d.z * k[10]);
+    d = vnorm(d);
+    return ray_make(v3(c->origin[0], c->origin[1], c->origin[2]), d);
+}
+
+static Col pixel_sample(const struct or_scene* s, uint32_t pixel, uint32_t sample, uint64_t seed, Counts* c) {
+    uint32_t x = pixel % (uint32_t)s->W, y = pixel / (uint32_t)s->W;
+    Pcg smp;
+    pcg_init(&smp, seed, ((uint64_t)pixel << 16) | sample);
+    Ray r = camera_ray(s, x + 0.5f, y + 0.5f);
+    Col thr = col(1.0f, 1.0f, 1.0f);
+    return path_trace(s, &r, &thr, 0, &smp, 1, c);
+}
+
+/* ------------------------------------------------------------------ public C API (ctypes) */
+typedef struct or_scene or_scene;
+
+or_scene* or_create(const rtg_scene_desc* d, int max_depth) {
+    if (!d || d->n_nodes == 0) return NULL;
+    or_scene* s = (or_scene*)calloc(1, sizeof(or_scene));
+    s->ntri = (int)d->n_tris;
+    s->nnode = (int)d->n_nodes;
+    s->nlight = (int)d->n_lights;
+    s->env_tex = d->env_texture;
+    s->max_depth = max_depth;
+    s->cam = d->camera;
+    s->W = (int)d->camera.width;
+    s->H = (int)d->camera.height;
+    s->tri = (Tri*)calloc((size_t)s->ntri + 1, sizeof(Tri));
+    for (int i = 0; i < s->ntri; ++i) { /* Triangle::init (Geometry.h:72-83) */
+        Tri* T = &s->tri[i];
+        for (int k = 0; k < 3; ++k) {
+            const float* p = d->positions + (size_t)i * 9 + k * 3;
+            const float* n = d->normals + (size_t)i * 9 + k * 3;
+            T->p[k] = v3(p[0], p[1], p[2]);
+            T->n[k] = v3(n[0], n[1], n[2]);
+            T->u[k] = d->uvs[(size_t)i * 6 + k * 2];
+            T->v[k] = d->uvs[(size_t)i * 6 + k * 2 + 1];
+        }
+        T->mat = d->material[i];
+        T->e1 = vsub(T->p[2], T->p[1]);
+        T->e2 = vsub(T->p[0], T->p[2]);
+        T->nrm = vnorm(vcross(T->e1, T->e2));
+        T->area = vlen(vcross(T->e1, T->e2)) * 0.5f;
+        T->d = vdot(T->nrm, T->p[0]);
+    }
+    s->node = (Node*)calloc((size_t)s->nnode, sizeof(Node));
+    for (int i = 0; i < s->nnode; ++i) {
+        const float* b = d->node_bounds + (size_t)i * 6;
+        const int32_t* L = d->node_links + (size_t)i * 4;
+        s->node[i].mn = v3(b[0], b[1], b[2]);
+        s->node[i].mx = v3(b[3], b[4], b[5]);
+        s->node[i].l = L[0];
+        s->node[i].r = L[1];
+        s->node[i].start = L[2];
+        s->node[i].end = L[3];
+    }
+    s->mat = (rtg_material*)calloc((size_t)d->n_materials + 1, sizeof(rtg_material));
+    memcpy(s->mat, d->materials, d->n_materials * sizeof(rtg_material));
+    size_t total = 0;
+    for (uint32_t i = 0; i < d->n_textures; ++i) total += (size_t)d->textures[i].width * d->textures[i].height * 3;
+    s->texels = (float*)malloc((total + 1) * sizeof(float));
+    s->tex = (Tex*)calloc((size_t)d->n_textures + 1, sizeof(Tex));
+    size_t off = 0;
+    for (uint32_t i = 0; i < d->n_textures; ++i) {
+        size_t n = (size_t)d->textures[i].width * d->textures[i].height * 3;
+        memcpy(s->texels + off, d->textures[i].texels, n * sizeof(float));
+        s->tex[i].w = d->textures[i].width;
+        s->tex[i].h = d->textures[i].height;
+        s->tex[i].t = s->texels + off;
+        off += n;
+    }
+    s->light = (int*)calloc((size_t)d->n_lights + 1, sizeof(int));
+    memcpy(s->light, d->lights, d->n_lights * sizeof(int));
+    return s;
+}
+
+void or_destroy(or_scene* s) {
+    if (!s) return;
+    free(s->tri); free(s->node); free(s->mat); free(s->tex); free(s->texels); free(s->light); free(s);
+}
+
+void or_set_max_depth(or_scene* s, int max_depth) { if (s) s->max_depth = max_depth; }
+
+/* Per-path radiance for an explicit (pixel, sample) list: out n*3. */
+int or_trace_paths(or_scene* s, const uint32_t* pixels, const uint32_t* samples, uint32_t n, uint64_t seed, float* out) {
+    if (!s || s->nlight <= 0) return -1;
+    for (uint32_t i = 0; i < n; ++i) {
+        Col L = pixel_sample(s, pixels[i], samples[i], seed, NULL);
+        out[i * 3] = L.r; out[i * 3 + 1] = L.g; out[i * 3 + 2] = L.b;
+    }
+    return 0;
+}
+
+/* RayTracer::render over tiles with a thread pool: for each sample (frame) in order, the
+ * 32x32 tiles are pulled from a shared counter by `threads` workers (pathTracerTileBased /
+ * getTileID), every pixel adds its path radiance to the film (renderTile + Film::splat).
+ * film is W*H*3 and accumulated in place. counts (optional) receives
+ * {paths, extension rays, shadow rays, node visits, triangle tests} when count != 0. */
+typedef struct {
+    or_scene* s;
+    const uint32_t* tiles;
+    uint32_t n_tiles;
+    uint32_t sample;
+    uint64_t seed;
+    float* film;
+    volatile uint32_t* next;
+    int count;
+    Counts cnt;
+} Job;
+
+static void render_tile(Job* j, uint32_t tile) {
+    const int TS = 32;
+    or_scene* s = j->s;
+    uint32_t tx = (uint32_t)(s->W + TS - 1) / TS;
+    uint32_t x0 = (tile % tx) * TS, y0 = (tile / tx) * TS;
+    for (uint32_t y = y0; y < y0 + TS && y < (uint32_t)s->H; ++y)
+        for (uint32_t x = x0; x < x0 + TS && x < (uint32_t)s->W; ++x) {
+            uint32_t pix = y * (uint32_t)s->W + x;
+            Col L = pixel_sample(s, pix, j->sample, j->seed, j->count ? &j->cnt : NULL);
+            float* f = j->film + (size_t)pix * 3;
+            f[0] = f[0] + L.r; f[1] = f[1] + L.g; f[2] = f[2] + L.b;
+        }
+}
+
+static void* worker(void* arg) {
+    Job* j = (Job*)arg;
+    for (;;) {
+        uint32_t k = __sync_fetch_and_add(j->next, 1u);
+        if (k >= j->n_tiles) break;
+        render_tile(j, j->tiles ? j->tiles[k] : k);
+    }
+    return NULL;
+}
+
+int or_render(or_scene* s, uint32_t first, uint32_t n_samples, uint64_t seed, const uint32_t* tiles, uint32_t n_tiles,
+              int threads, float* film, uint64_t* counts, int count) {
+    if (!s || !film || s->nlight <= 0) return -1;
+    const int TS = 32;
+    uint32_t ntiles_all = (uint32_t)((s->W + TS - 1) / TS) * (uint32_t)((s->H + TS - 1) / TS);
+    uint32_t nt = tiles ? n_tiles : ntiles_all;
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    Job jobs[256];
+    pthread_t th[256];
+    Counts total = {0, 0, 0, 0};
+    for (uint32_t smp = first; smp < first + n_samples; ++smp) {
+        volatile uint32_t next = 0;
+        for (int t = 0; t < threads; ++t) {
+            memset(&jobs[t], 0, sizeof(Job));
+            jobs[t].s = s; jobs[t].tiles = tiles; jobs[t].n_tiles = nt; jobs[t].sample = smp;
+            jobs[t].seed = seed; jobs[t].film = film; jobs[t].next = &next; jobs[t].count = count;
+        }
+        if (threads == 1) worker(&jobs[0]);
+        else {
+            for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, worker, &jobs[t]);
+            for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);
+        }
+        for (int t = 0; t < threads; ++t) {
+            total.ext_rays += jobs[t].cnt.ext_rays; total.shadow_rays += jobs[t].cnt.shadow_rays;
+            total.nodes += jobs[t].cnt.nodes; total.tris += jobs[t].cnt.tris;
+        }
+    }
+    if (counts) {
+        uint64_t npix = 0;
+        for (uint32_t k = 0; k < nt; ++k) {
+            uint32_t t = tiles ? tiles[k] : k;
+            uint32_t tx = (uint32_t)(s->W + TS - 1) / TS;
+            uint32_t x0 = (t % tx) * TS, y0 = (t / tx) * TS;
+            uint32_t w = (uint32_t)s->W - x0 < (uint32_t)TS ? (uint32_t)s->W - x0 : (uint32_t)TS;
+            uint32_t h = (uint32_t)s->H - y0 < (uint32_t)TS ? (uint32_t)s->H - y0 : (uint32_t)TS;
+            npix += (uint64_t)w * h;
+        }
+        counts[0] = npix * n_samples;
+        counts[1] = total.ext_rays; counts[2] = total.shadow_rays; counts[3] = total.nodes; counts[4] = total.tris;
+    }
+    return 0;
+}
+
+/* Ray queries with the reference traversal (IntersectionData / Scene::visible semantics).
+ * rays: n*8 (o.xyz, tmax, dir.xyz, pad); hits n*4 (t, id bits, alpha, beta). */
+int or_trace_closest(or_scene* s, const float* rays, uint32_t n, float* hits) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* q = rays + (size_t)i * 8;
+        Ray r = ray_make(v3(q[0], q[1], q[2]), v3(q[4], q[5], q[6]));
+        Isect is = scene_traverse(s, &r, NULL);
+        int32_t id = is.t < FLT_MAX ? is.id : -1;
+        hits[i * 4] = is.t;
+        memcpy(&hits[i * 4 + 1], &id, 4);
+        hits[i * 4 + 2] = is.t < FLT_MAX ? is.alpha : 0.0f;
+        hits[i * 4 + 3] = is.t < FLT_MAX ? is.beta : 0.0f;
+    }
+    return 0;
+}
+
+int or_trace_visible(or_scene* s, const float* rays, uint32_t n, int32_t* vis) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* q = rays + (size_t)i * 8;
+        Ray r = ray_make(v3(q[0], q[1], q[2]), v3(q[4], q[5], q[6]));
+        vis[i] = traverse_visible(s, 0, &r, q[3], NULL);
+    }
+    return 0;
+}
+
+/* Camera rays for pixel centres: out n*6 (o.xyz, dir.xyz). */
+int or_camera_rays(or_scene* s, const uint32_t* pixels, uint32_t n, float* out) {
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t x = pixels[i] % (uint32_t)s->W, y = pixels[i] / (uint32_t)s->W;
+        Ray r = camera_ray(s, x + 0.5f, y + 0.5f);
+        out[i * 6] = r.o.x; out[i * 6 + 1] = r.o.y; out[i * 6 + 2] = r.o.z;
+        out[i * 6 + 3] = r.dir.x; out[i * 6 + 4] = r.dir.y; out[i * 6 + 5] = r.dir.z;
+    }
+    return 0;
+}
+
+/* Scalar probes of the shared math (for tests). */
+float or_acosf(float x) { return O_ACOSF(x); }
+float or_sinf(float x) { return O_SINF(x); }
+float or_cosf(float x) { return O_COSF(x); }
+float or_atan2f(float y, float x) { return O_ATAN2F(y, x); }

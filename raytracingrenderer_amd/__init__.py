@@ -1,0 +1,9 @@
+"""raytracingrenderer_amd — MI355X-native wavefront path tracer with RTBase's host API.
+
+The hot path (RayTracer::render) runs as HIP kernels in lib/librtg.so behind include/rtg.h;
+scene loading / BVH build / HDR output run in lib/librth.so behind include/rth.h.
+"""
+from .renderer import (NativeError, RayTracer, Scene, loadScene, read_hdr, save_hdr,  # noqa: F401
+                       write_synthetic_scene)
+
+__all__ = ["RayTracer", "Scene", "loadScene", "save_hdr", "read_hdr", "write_synthetic_scene", "NativeError"]

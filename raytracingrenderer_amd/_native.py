@@ -1,0 +1,131 @@
+"""ctypes bindings for the two native libraries (include/rtg.h, include/rth.h).
+
+No fallback: if librtg.so / librth.so are missing or fail to load, import of the bindings
+raises. Build them with `python -m raytracingrenderer_amd.build` (or __graft_entry__.build()).
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(_HERE, "lib")
+
+RTG_MAT_DIFFUSE, RTG_MAT_LAMBERT, RTG_MAT_MIRROR, RTG_MAT_GLASS = 0, 1, 2, 3
+RTG_OPT_CULL, RTG_OPT_COUNT, RTG_OPT_TIMING = 1, 2, 4
+
+f32p = C.POINTER(C.c_float)
+u32p = C.POINTER(C.c_uint32)
+i32p = C.POINTER(C.c_int32)
+
+
+class rtg_camera(C.Structure):
+    _fields_ = [("inv_proj", C.c_float * 16), ("camera", C.c_float * 16), ("origin", C.c_float * 3),
+                ("width", C.c_float), ("height", C.c_float)]
+
+
+class rtg_material(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("two_sided", C.c_int32), ("texture", C.c_int32),
+                ("int_ior", C.c_float), ("ext_ior", C.c_float), ("emission", C.c_float * 3)]
+
+
+class rtg_texture(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("texels", f32p)]
+
+
+class rtg_scene_desc(C.Structure):
+    _fields_ = [("n_tris", C.c_uint32), ("positions", f32p), ("normals", f32p), ("uvs", f32p),
+                ("material", u32p), ("n_nodes", C.c_uint32), ("node_bounds", f32p),
+                ("node_links", i32p), ("n_materials", C.c_uint32),
+                ("materials", C.POINTER(rtg_material)), ("n_textures", C.c_uint32),
+                ("textures", C.POINTER(rtg_texture)), ("env_texture", C.c_int32),
+                ("n_lights", C.c_uint32), ("lights", i32p), ("camera", rtg_camera)]
+
+
+class rtg_stats(C.Structure):
+    _fields_ = [("paths", C.c_uint64), ("extension_rays", C.c_uint64), ("shadow_rays", C.c_uint64),
+                ("node_visits", C.c_uint64), ("tri_tests", C.c_uint64), ("render_ms", C.c_double),
+                ("extend_ms", C.c_double), ("shadow_ms", C.c_double), ("shade_ms", C.c_double)]
+
+
+class rth_load_options(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("skip_missing", C.c_int32),
+                ("bvh_threads", C.c_int32), ("envmap", C.c_char_p)]
+
+
+class rth_scene_info(C.Structure):
+    _fields_ = [("n_tris", C.c_uint32), ("n_nodes", C.c_uint32), ("n_materials", C.c_uint32),
+                ("n_textures", C.c_uint32), ("n_lights", C.c_uint32), ("bvh_depth", C.c_uint32),
+                ("width", C.c_int32), ("height", C.c_int32), ("env_in_lights", C.c_int32),
+                ("dropped_instances", C.c_uint32), ("load_ms", C.c_double), ("bvh_ms", C.c_double),
+                ("bounds_min", C.c_float * 3), ("bounds_max", C.c_float * 3)]
+
+
+RTG_EXPORTS = [
+    ("rtg_abi_version", C.c_int32, []),
+    ("rtg_last_error", C.c_char_p, []),
+    ("rtg_device_count", C.c_int, [i32p]),
+    ("rtg_create", C.c_int, [C.c_int, C.POINTER(rtg_scene_desc), C.POINTER(C.c_void_p)]),
+    ("rtg_destroy", None, [C.c_void_p]),
+    ("rtg_set_options", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_uint32]),
+    ("rtg_render", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32]),
+    ("rtg_render_async", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32, C.c_void_p]),
+    ("rtg_synchronize", C.c_int, [C.c_void_p]),
+    ("rtg_film_read", C.c_int, [C.c_void_p, f32p, u32p]),
+    ("rtg_film_copy_device", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("rtg_film_load", C.c_int, [C.c_void_p, f32p, C.c_uint32]),
+    ("rtg_clear", C.c_int, [C.c_void_p]),
+    ("rtg_get_stats", C.c_int, [C.c_void_p, C.POINTER(rtg_stats)]),
+    ("rtg_trace_closest", C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
+    ("rtg_trace_visible", C.c_int, [C.c_void_p, f32p, C.c_uint32, i32p]),
+]
+
+RTH_EXPORTS = [
+    ("rth_last_error", C.c_char_p, []),
+    ("rth_load_scene", C.c_int, [C.c_char_p, C.POINTER(rth_load_options), C.POINTER(C.c_void_p)]),
+    ("rth_free_scene", None, [C.c_void_p]),
+    ("rth_scene_desc", C.POINTER(rtg_scene_desc), [C.c_void_p]),
+    ("rth_scene_get_info", C.c_int, [C.c_void_p, C.POINTER(rth_scene_info)]),
+    ("rth_scene_permutation", C.c_int, [C.c_void_p, u32p]),
+    ("rth_save_hdr", C.c_int, [C.c_char_p, C.c_int32, C.c_int32, f32p, C.c_uint32]),
+    ("rth_write_hdr", C.c_int, [C.c_char_p, C.c_int32, C.c_int32, f32p]),
+    ("rth_read_hdr", C.c_int, [C.c_char_p, i32p, i32p, C.POINTER(f32p)]),
+    ("rth_read_png", C.c_int, [C.c_char_p, i32p, i32p, i32p, C.POINTER(C.POINTER(C.c_uint8))]),
+    ("rth_free", None, [C.c_void_p]),
+    ("rth_write_synthetic", C.c_int, [C.c_char_p, C.c_uint32, C.c_uint64, C.c_int32, C.c_int32]),
+]
+
+
+def _bind(lib, exports):
+    for name, res, args in exports:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_rth = None
+_rtg = None
+
+
+def rth():
+    global _rth
+    if _rth is None:
+        path = os.path.join(LIB_DIR, "librth.so")
+        if not os.path.exists(path):
+            raise ImportError("librth.so not built (run raytracingrenderer_amd.build)")
+        _rth = _bind(C.CDLL(path), RTH_EXPORTS)
+    return _rth
+
+
+def rtg():
+    """The HIP library. Raises if missing: there is no CPU fallback for the render path."""
+    global _rtg
+    if _rtg is None:
+        path = os.path.join(LIB_DIR, "librtg.so")
+        if not os.path.exists(path):
+            raise ImportError("librtg.so not built (run raytracingrenderer_amd.build)")
+        _rtg = _bind(C.CDLL(path, mode=C.RTLD_GLOBAL), RTG_EXPORTS)
+    return _rtg
+
+
+def ptr(arr, ctype):
+    return arr.ctypes.data_as(C.POINTER(ctype))

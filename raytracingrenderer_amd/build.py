@@ -1,0 +1,117 @@
+"""In-tree native build for the MI355X path tracer.
+
+Outputs (git-ignored, shipped to the GPU box with the source snapshot):
+  raytracingrenderer_amd/lib/librth.so       host front-end (C++17, g++)         include/rth.h
+  raytracingrenderer_amd/lib/librtg.so       HIP kernels + C-ABI (hipcc gfx950)  include/rtg.h
+  raytracingrenderer_amd/lib/rtg_render      headless CLI (-scene -SPP -outputFilename)
+  oracle/_build/liboracle_rtm.so             test-only CPU restatement, shared math
+  oracle/_build/liboracle_libm.so            test-only CPU restatement, C-library math
+Every float-producing unit is compiled with -ffp-contract=off (bit-faithful arithmetic).
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "raytracingrenderer_amd")
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "lib")
+ORACLE = os.path.join(ROOT, "oracle")
+ORACLE_BUILD = os.path.join(ORACLE, "_build")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("RTG_ARCH", "gfx950")
+
+HOST_SRC = ["host/image_io.cpp", "host/gem_json.cpp", "host/scene_front.cpp"]
+DEVICE_SRC = ["device/rtg_kernels.hip"]
+
+
+def _newer(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _deps(paths):
+    extra = [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
+    for sub in ("host", "device"):
+        d = os.path.join(CSRC, sub)
+        extra += [os.path.join(d, f) for f in os.listdir(d) if f.endswith(".h")]
+    return list(paths) + extra
+
+
+def _run(cmd, cwd=None):
+    r = subprocess.run(cmd, cwd=cwd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("build failed: " + " ".join(cmd))
+    return r
+
+
+def build_host(force=False):
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, "librth.so")
+    src = [os.path.join(CSRC, s) for s in HOST_SRC]
+    if force or _newer(out, _deps(src)):
+        _run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fPIC", "-shared", "-Wall",
+              "-o", out] + src + ["-lz", "-lpthread"])
+    return out
+
+
+def build_device(force=False):
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, "librtg.so")
+    src = [os.path.join(CSRC, s) for s in DEVICE_SRC]
+    if force or _newer(out, _deps(src)):
+        _run([HIPCC, "--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-std=c++17",
+              "-fPIC", "-shared", "-o", out] + src)
+    return out
+
+
+def build_cli(force=False):
+    out = os.path.join(LIB, "rtg_render")
+    src = [os.path.join(CSRC, "host", "cli.cpp")]
+    if not os.path.exists(src[0]):
+        return None
+    if force or _newer(out, _deps(src) + [os.path.join(LIB, "librth.so")]):
+        _run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-o", out] + src +
+             ["-L" + LIB, "-lrth", "-lrtg", "-Wl,-rpath,$ORIGIN", "-ldl"])
+    return out
+
+
+def build_oracle(force=False):
+    """Test infrastructure: the C restatement (checker / cpu_baseline only)."""
+    os.makedirs(ORACLE_BUILD, exist_ok=True)
+    src = os.path.join(ORACLE, "rt_oracle.c")
+    outs = []
+    for flavour, libm in (("rtm", "0"), ("libm", "1")):
+        out = os.path.join(ORACLE_BUILD, "liboracle_%s.so" % flavour)
+        if force or _newer(out, _deps([src])):
+            _run(["gcc", "-std=c11", "-O2", "-ffp-contract=off", "-fPIC", "-shared", "-D_GNU_SOURCE",
+                  "-DORACLE_LIBM=" + libm, "-o", out, src, "-lm", "-lpthread"])
+        outs.append(out)
+    return outs
+
+
+def build_ref(force=False):
+    """oracle/_ref: the reference's own compilable headers, only when /root/reference exists."""
+    mk = os.path.join(ORACLE, "ref", "Makefile")
+    if not os.path.isdir("/root/reference/RTBase") or not os.path.exists(mk):
+        return None
+    _run(["make", "-s", "-C", os.path.join(ORACLE, "ref")] + (["-B"] if force else []))
+    return os.path.join(ORACLE, "_ref", "libref.so")
+
+
+def build_all(force=False, device=True):
+    build_host(force)
+    if device:
+        build_device(force)
+    build_cli(force)
+    build_oracle(force)
+    build_ref(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv, device="--no-device" not in sys.argv)
+    print("ok")

@@ -1,0 +1,263 @@
+// rtg_dev.h — device data layout and reference-faithful device math for the wavefront tracer.
+//
+// Every helper here restates an RTBase expression with the same IEEE operation order
+// (this TU is compiled with -ffp-contract=off; gfx950 f32 '/' and sqrtf are correctly rounded):
+//   Vec3/Colour ops         RTBase/Core.h:16-195
+//   Frame                   RTBase/Core.h:507-542
+//   Ray::init               RTBase/Geometry.h:21-26 (invDir = 1/dir)
+//   AABB::rayAABB           RTBase/Geometry.h:159-184 (Min/Max ternaries, std::max/min)
+//   Triangle::rayIntersect  RTBase/Geometry.h:89-105 (plane test)
+//   Texture::sample         RTBase/Imaging.h:72-94 (bilinear, integer wrap)
+//   SamplingDistributions   RTBase/Sampling.h:44-69 (binary64 islands around M_PI)
+//   fresnelDielectric       RTBase/Materials.h:55-77
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../../include/rtg_math.h"
+
+#define RTG_D __device__ __forceinline__
+#define RTG_FLT_MAX 3.40282347e+38f
+#define RTG_EPS 1e-4f                    // EPSILON, Geometry.h:60
+#define RTG_PI_F 3.14159274f             // (float)M_PI, as in Colour / M_PI (Materials.h:131)
+#define RTG_EXIT ((int)0x80000000)       // traversal sentinel (never a valid child word)
+
+namespace rtgd {
+
+struct v3 { float x, y, z; };
+RTG_D v3 mk(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+RTG_D v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+RTG_D v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+RTG_D v3 mul(v3 a, v3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+RTG_D v3 muls(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+RTG_D v3 divs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+RTG_D v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }
+RTG_D float dot(v3 a, v3 b) { return ((a.x * b.x) + (a.y * b.y)) + (a.z * b.z); }
+RTG_D v3 cross(v3 a, v3 b) {
+    return mk((a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x));
+}
+RTG_D float length_sq(v3 a) { return ((a.x * a.x) + (a.y * a.y)) + (a.z * a.z); }
+RTG_D v3 normalize(v3 a) {
+    float l = 1.0f / sqrtf(((a.x * a.x) + (a.y * a.y)) + (a.z * a.z));
+    return mk(a.x * l, a.y * l, a.z * l);
+}
+RTG_D float lum(v3 c) { return ((0.2126f * c.x) + (0.7152f * c.y)) + (0.0722f * c.z); }
+// windows.h max/min macro semantics used by Renderer.h (max(NaN, 0) -> 0)
+RTG_D float wmax(float a, float b) { return a > b ? a : b; }
+RTG_D float wmin(float a, float b) { return a < b ? a : b; }
+// std::max / std::min (libstdc++): max(a,b) = (a < b) ? b : a ; min(a,b) = (b < a) ? b : a
+RTG_D float smax(float a, float b) { return (a < b) ? b : a; }
+RTG_D float smin(float a, float b) { return (b < a) ? b : a; }
+
+struct frame { v3 u, v, w; };
+RTG_D frame frame_from(v3 n) {  // Frame::fromVector
+    frame f;
+    f.w = normalize(n);
+    if (fabsf(f.w.x) > fabsf(f.w.y)) {
+        float l = 1.0f / sqrtf(f.w.x * f.w.x + f.w.z * f.w.z);
+        f.u = mk(f.w.z * l, 0.0f, -f.w.x * l);
+    } else {
+        float l = 1.0f / sqrtf(f.w.y * f.w.y + f.w.z * f.w.z);
+        f.u = mk(0.0f, f.w.z * l, -f.w.y * l);
+    }
+    f.v = cross(f.w, f.u);
+    return f;
+}
+RTG_D v3 to_local(const frame& f, v3 a) { return mk(dot(a, f.u), dot(a, f.v), dot(a, f.w)); }
+RTG_D v3 to_world(const frame& f, v3 a) {
+    return add(add(muls(f.u, a.x), muls(f.v, a.y)), muls(f.w, a.z));
+}
+
+// ------------------------------------------------------------------ device scene layout
+// Internal BVH2 node, child-pair form: both child boxes live in the parent so one 64-byte fetch
+// (4 x dwordx4) tests both. Child word: >= 0 internal node index; < 0 leaf, ~c = start*2 + (n-1).
+struct __align__(16) DevNode {
+    float4 a;  // lmin.x lmin.y lmin.z lmax.x
+    float4 b;  // lmax.y lmax.z rmin.x rmin.y
+    float4 c;  // rmin.z rmax.x rmax.y rmax.z
+    int4 d;    // left word, right word, -, -
+};
+// Hot intersection record (64 B): exactly the operands of Triangle::rayIntersect.
+struct __align__(16) DevTri {
+    float4 nd;    // n.xyz, d
+    float4 v1i;   // vertices[1].p, invArea = 1/Dot(e1 x e2, n)
+    float4 v2;    // vertices[2].p, -
+    float4 e2;    // e2 = v0 - v2, -   (e1 = v2 - v1 is recomputed: same float op)
+};
+// Cold shading record (64 B): vertex normals, uvs, material.
+struct __align__(16) DevShade {
+    float4 a;  // n0.xyz n1.x
+    float4 b;  // n1.yz n2.xy
+    float4 c;  // n2.z u0 v0 u1
+    float4 d;  // v1 u2 v2 material(int bits)
+};
+struct __align__(16) DevMat {
+    int kind, two_sided, tex, is_light;
+    float int_ior, ext_ior, pad0, pad1;
+    float4 emission;
+};
+struct __align__(16) DevLight {
+    float4 v0a;  // v0.xyz, area       (area light)
+    float4 v1t;  // v1.xyz, type bits  (0 area, 1 environment)
+    float4 v2;   // v2.xyz
+    float4 gn;   // gNormal.xyz        (Triangle::gNormal)
+    float4 em;   // emission rgb
+};
+struct DevTex { int off, w, h, pad; };
+
+struct DevCamera {
+    float ip[16];  // inverse projection
+    float cm[16];  // camera
+    float ox, oy, oz, width, height;
+};
+
+struct SceneView {
+    const DevNode* nodes;
+    const DevTri* tris;
+    const DevShade* shade;
+    const DevMat* mats;
+    const DevLight* lights;
+    const DevTex* texinfo;
+    const float* texels;
+    int n_lights;
+    int env_tex;         // -1: BackgroundColour(0)
+    int root_word;       // child word of the root (RTG_EXIT if no triangles)
+    float root_box[6];   // bounds of the reference root node
+    float cull_scale;    // scene magnitude used for the conservative cull inflation
+};
+
+// ------------------------------------------------------------------ Texture::sample
+RTG_D v3 texel(const float* t, int i) { return mk(t[i * 3 + 0], t[i * 3 + 1], t[i * 3 + 2]); }
+RTG_D v3 tex_sample(const SceneView& s, int tex, float tu, float tv) {
+    DevTex ti = s.texinfo[tex];
+    const float* T = s.texels + (size_t)ti.off * 3;
+    float au = fabsf(tu), av = fabsf(tv);
+    float u = smax(0.0f, au) * (float)ti.w;
+    float v = smax(0.0f, av) * (float)ti.h;
+    int x = (int)floorf(u);
+    int y = (int)floorf(v);
+    float fu = u - (float)x;
+    float fv = v - (float)y;
+    float w0 = (1.0f - fu) * (1.0f - fv);
+    float w1 = fu * (1.0f - fv);
+    float w2 = (1.0f - fu) * fv;
+    float w3 = fu * fv;
+    x = x % ti.w;
+    y = y % ti.h;
+    int x1 = (x + 1) % ti.w, y1 = (y + 1) % ti.h;
+    v3 s0 = texel(T, y * ti.w + x), s1 = texel(T, y * ti.w + x1);
+    v3 s2 = texel(T, y1 * ti.w + x), s3 = texel(T, y1 * ti.w + x1);
+    return add(add(add(muls(s0, w0), muls(s1, w1)), muls(s2, w2)), muls(s3, w3));
+}
+
+// ------------------------------------------------------------------ sampling (Sampling.h)
+RTG_D v3 spherical_to_world(float theta, float phi) {  // Core.h:547-550
+    return mk(rtm_cosf(phi) * rtm_sinf(theta), rtm_sinf(phi) * rtm_sinf(theta), rtm_cosf(theta));
+}
+RTG_D v3 cosine_sample_hemisphere(float r1, float r2) {
+    float theta = rtm_acosf(sqrtf(r1));
+    float phi = (float)((2.0 * RTM_PI) * (double)r2);  // 2.0f * M_PI * r2 in binary64
+    return spherical_to_world(theta, phi);
+}
+RTG_D v3 uniform_sample_sphere(float r1, float r2) {
+    float theta = rtm_acosf(1.0f - 2.0f * r1);
+    float phi = (float)((2.0 * RTM_PI) * (double)r2);
+    return spherical_to_world(theta, phi);
+}
+RTG_D float uniform_sphere_pdf() { return (float)(1.0 / (4.0 * RTM_PI)); }
+
+// EnvironmentMap::evaluate (Lights.h:150-157)
+RTG_D v3 env_eval(const SceneView& s, v3 wi) {
+    float u = rtm_atan2f(wi.z, wi.x);
+    u = (u < 0.0f) ? (float)((double)u + 2.0 * RTM_PI) : u;
+    u = (float)((double)u / (2.0 * RTM_PI));
+    float v = (float)((double)rtm_acosf(wi.y) / RTM_PI);
+    return tex_sample(s, s.env_tex, u, v);
+}
+RTG_D v3 background(const SceneView& s, v3 dir) {
+    if (s.env_tex < 0) return mk(0.0f, 0.0f, 0.0f);  // BackgroundColour(0,0,0)::evaluate
+    return env_eval(s, dir);
+}
+
+// fresnelDielectric (Materials.h:55-77); returns R, writes wt when not TIR.
+RTG_D float fresnel_dielectric(float cos_i, float ior_int, float ior_ext, v3& wt, v3 wol) {
+    float ior = ior_int / ior_ext;
+    float sin_i = sqrtf(1 - (cos_i * cos_i));
+    float sin_t = ior * sin_i;
+    float ior2sin2 = (ior * ior) * (1 - (cos_i * cos_i));
+    if (ior2sin2 > 1.0f) return 1.0f;
+    float cos_t = sqrtf(1 - (sin_t * sin_t));
+    wt = mk(-ior * wol.x, -ior * wol.y, -cos_t);
+    float fpa = (cos_i - ior * cos_t) / (cos_i + ior * cos_t);
+    float fpe = (ior * cos_i - cos_t) / (ior * cos_i + ior * cos_t);
+    float avg = ((fpa * fpa) + (fpe * fpe)) * 0.5f;
+    return smax(0.0f, smin(1.0f, avg));  // clamp(avg, 0, 1) = max(0, min(1, avg))
+}
+
+// ------------------------------------------------------------------ RNG
+RTG_D uint32_t pcg_step(uint64_t& s, uint64_t inc) {
+    uint64_t old = s;
+    s = old * 6364136223846793005ull + inc;
+    uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    uint32_t rot = (uint32_t)(old >> 59u);
+    return (xs >> rot) | (xs << ((0u - rot) & 31u));
+}
+RTG_D uint64_t pcg_inc(uint32_t pixel, uint32_t sample) {
+    uint64_t seq = ((uint64_t)pixel << 16) | (uint64_t)sample;
+    return (seq << 1u) | 1u;
+}
+RTG_D uint64_t pcg_seed(uint64_t seed, uint64_t inc) {
+    uint64_t s = 0;
+    pcg_step(s, inc);
+    s += seed;
+    pcg_step(s, inc);
+    return s;
+}
+RTG_D float pcg_next(uint64_t& s, uint64_t inc) {
+    return (float)(pcg_step(s, inc) >> 8) * (1.0f / 16777216.0f);
+}
+
+// ------------------------------------------------------------------ intersection
+// AABB::rayAABB with the reference's exact arithmetic; returns pass/fail.
+RTG_D bool slab_exact(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, v3 o, v3 inv) {
+    float ax = (mnx - o.x) * inv.x, ay = (mny - o.y) * inv.y, az = (mnz - o.z) * inv.z;
+    float bx = (mxx - o.x) * inv.x, by = (mxy - o.y) * inv.y, bz = (mxz - o.z) * inv.z;
+    float ex = ax < bx ? ax : bx, ey = ay < by ? ay : by, ez = az < bz ? az : bz;  // Min
+    float xx = ax > bx ? ax : bx, xy = ay > by ? ay : by, xz = az > bz ? az : bz;  // Max
+    float te = smax(smax(ex, ey), ez);
+    float tx = smin(smin(xx, xy), xz);
+    return !(tx < te || tx < 0);
+}
+// Conservative entry distance of the box inflated by delta (position space). Used only to
+// skip boxes that cannot contain a hit closer than the current one; never to accept.
+RTG_D float slab_cull_entry(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                            v3 o, v3 inv, float delta) {
+    float nx = (inv.x >= 0.0f ? mnx - delta : mxx + delta);
+    float ny = (inv.y >= 0.0f ? mny - delta : mxy + delta);
+    float nz = (inv.z >= 0.0f ? mnz - delta : mxz + delta);
+    float cx = (nx - o.x) * inv.x, cy = (ny - o.y) * inv.y, cz = (nz - o.z) * inv.z;
+    return fmaxf(fmaxf(cx, cy), cz);  // fmaxf drops NaN -> conservative
+}
+
+// Triangle::rayIntersect; t,u,v written only on success.
+RTG_D bool tri_intersect(const DevTri& T, v3 o, v3 d, float& t, float& u, float& v) {
+    v3 n = mk(T.nd.x, T.nd.y, T.nd.z);
+    float denom = dot(n, d);
+    if (denom == 0) return false;
+    float tt = (T.nd.w - dot(n, o)) / denom;
+    if (tt < 0) return false;
+    v3 p = add(o, muls(d, tt));
+    v3 v1 = mk(T.v1i.x, T.v1i.y, T.v1i.z), v2 = mk(T.v2.x, T.v2.y, T.v2.z);
+    v3 e1 = sub(v2, v1), e2 = mk(T.e2.x, T.e2.y, T.e2.z);
+    float inv_area = T.v1i.w;
+    float uu = dot(cross(e1, sub(p, v1)), n) * inv_area;
+    if (uu < 0 || uu > 1.0f) return false;
+    float vv = dot(cross(e2, sub(p, v2)), n) * inv_area;
+    if (vv < 0 || (uu + vv) > 1.0f) return false;
+    t = tt;
+    u = uu;
+    v = vv;
+    return true;
+}
+
+}  // namespace rtgd

@@ -1,0 +1,1034 @@
+// rtg_kernels.hip — MI355X (gfx950) wavefront path tracer: kernels + the C-ABI of include/rtg.h.
+//
+// One RayTracer::render() (RTBase/Renderer.h:876) = one sample for every pixel. Here a "chunk" is
+// ns samples x npix pixels = P paths in flight, advanced bounce by bounce:
+//
+//   k_generate        Camera::generateRay (Scene.h:43-54) at pixel centres, PCG32 seed, path state
+//   for b in 0 .. max_depth+1:                                   (pathTrace recursion, depth = b)
+//     k_trace<closest> Scene::traverse  (Scene.h:107-130, Geometry.h:399-434)
+//     k_shade          calculateShadingData + emission + computeDirect (NEE sample, shadow ray)
+//                      + Russian roulette + BSDF::sample + throughput (Renderer.h:328-392, 423-473)
+//                      -> compacts continuing paths into the next extension queue and NEE rays
+//                      into the shadow queue (wave ballot + mbcnt prefix, one atomic per wave)
+//     k_trace<any>     Scene::visible   (Scene.h:161-169, Geometry.h:435-462)
+//   k_accumulate      right-nested radiance sum d0 + (d1 + (... + dk)) (Renderer.h:388) per path,
+//                      then film += L in sample order (Film::splat, Imaging.h:209-232)
+//
+// Exactness: each path's result is independent of queue order and of traversal order. Closest hit
+// returns the (t, triangle index) lexicographic minimum over the reference's reachable triangles,
+// which is what the reference's left-first DFS with strict '<' keeps; box tests use the reference's
+// exact slab arithmetic, and distance culling only removes boxes whose conservatively inflated entry
+// is beyond the current hit.
+#include "rtg_dev.h"
+#include "../../../include/rtg.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace rtgd;
+
+#define RTG_TB 256          // threads per block (4 waves)
+#define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (24 KB per block)
+#define RTG_CULL_REL 1.52587890625e-05f  // 2^-16 relative inflation for distance culling
+
+struct __align__(16) ExtRay { float4 o; float4 d; };            // o.w = path id bits
+struct __align__(16) ShadowRay { float4 o; float4 d; float4 c; }; // o.w = maxT, d.w = path id, c = NEE value
+struct __align__(16) Counters { unsigned n_ext, n_shadow, f_ext, f_shadow, f_shade, pad0, pad1, pad2; };
+
+struct TraceIO {
+    const ExtRay* ext;         // closest-hit input
+    const ShadowRay* sh;       // any-hit input
+    const unsigned* count;     // number of rays (device)
+    unsigned* fetch;           // work counter (device, zeroed)
+    float4* hits;              // closest-hit output
+    float4* contrib;           // any-hit: write ShadowRay.c to contrib[pid] when visible
+    int* visible;              // any-hit query output (instead of contrib)
+    int* ovf;                  // global stack overflow [level][thread]
+    unsigned long long* stats; // [0] node visits, [1] triangle tests (COUNT builds)
+    int cull;
+};
+
+struct ChunkArgs {
+    const unsigned* pixlist;   // local pixel -> pixel index (y*W + x)
+    unsigned npix, ns, s0, P;
+    unsigned long long seed;
+    int max_depth;
+    DevCamera cam;
+};
+
+struct PathBufs {
+    float4* thr;               // [P] throughput
+    unsigned long long* rng;   // [P] PCG state
+    int* meta;                 // [P] nterms | canHitLight << 8
+    float4* contrib;           // [maxb][P] per-vertex radiance terms
+    ExtRay* q[2];              // extension queues (ping-pong)
+    float4* hits;              // [P]
+    ShadowRay* shq;            // [P]
+    Counters* ctr;             // [maxb + 1]
+};
+
+static __device__ __forceinline__ int lane_id() { return __lane_id(); }
+static __device__ __forceinline__ unsigned prefix_lt(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+// ------------------------------------------------------------------ traversal
+template <bool ANY, bool COUNT>
+__global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
+    __shared__ int stk[RTG_STACK][RTG_TB];
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const unsigned gthreads = gridDim.x * blockDim.x;
+    const unsigned gtid = blockIdx.x * blockDim.x + tid;
+    const unsigned n = *io.count;
+    unsigned long long c_nodes = 0, c_tris = 0;
+    for (;;) {
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(io.fetch, 64u);
+        base = __shfl(base, 0);
+        if (base >= n) break;
+        const unsigned i = base + lane;
+        if (i < n) {
+            v3 o, d;
+            float tbest;
+            float4 shc;
+            int pid = 0;
+            if (ANY) {
+                ShadowRay r = io.sh[i];
+                o = mk(r.o.x, r.o.y, r.o.z);
+                d = mk(r.d.x, r.d.y, r.d.z);
+                tbest = r.o.w;
+                pid = __float_as_int(r.d.w);
+                shc = r.c;
+            } else {
+                ExtRay r = io.ext[i];
+                o = mk(r.o.x, r.o.y, r.o.z);
+                d = mk(r.d.x, r.d.y, r.d.z);
+                tbest = RTG_FLT_MAX;
+            }
+            const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // Ray::init
+            const float omag = s.cull_scale + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+            const float dmag = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+            float delta = RTG_CULL_REL * (omag + (tbest < RTG_FLT_MAX ? tbest * dmag : 0.0f));
+            int bid = -1;
+            float bu = 0.0f, bv = 0.0f;
+            bool occluded = false;
+            const float* rb = s.root_box;
+            int cur = slab_exact(rb[0], rb[1], rb[2], rb[3], rb[4], rb[5], o, inv) ? s.root_word : RTG_EXIT;
+            int sp = 0;
+            while (cur != RTG_EXIT) {
+                if (cur >= 0) {
+                    if (COUNT) c_nodes += 2;
+                    const DevNode nd = s.nodes[cur];
+                    bool hl = slab_exact(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, o, inv);
+                    bool hr = slab_exact(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, o, inv);
+                    float el = slab_cull_entry(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, o, inv, delta);
+                    float er = slab_cull_entry(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, o, inv, delta);
+                    if (io.cull) {
+                        hl = hl && !(el > tbest);
+                        hr = hr && !(er > tbest);
+                    }
+                    if (hl && hr) {
+                        const bool lfirst = !(er < el);
+                        const int nearw = lfirst ? nd.d.x : nd.d.y;
+                        const int farw = lfirst ? nd.d.y : nd.d.x;
+                        if (sp < RTG_STACK) stk[sp][tid] = farw;
+                        else io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid] = farw;
+                        ++sp;
+                        cur = nearw;
+                    } else if (hl) {
+                        cur = nd.d.x;
+                    } else if (hr) {
+                        cur = nd.d.y;
+                    } else if (sp == 0) {
+                        cur = RTG_EXIT;
+                    } else {
+                        --sp;
+                        cur = sp < RTG_STACK ? stk[sp][tid] : io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
+                    }
+                } else {
+                    const int code = ~cur;
+                    const int start = code >> 1;
+                    const int cnt = (code & 1) + 1;
+                    for (int k = 0; k < cnt; ++k) {
+                        const int tri = start + k;
+                        if (COUNT) c_tris += 1;
+                        const DevTri T = s.tris[tri];
+                        float t, u, v;
+                        if (tri_intersect(T, o, d, t, u, v)) {
+                            if (ANY) {
+                                if (!(t >= tbest || t <= RTG_EPS)) occluded = true;
+                            } else if (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid))) {
+                                tbest = t;
+                                bid = tri;
+                                bu = u;
+                                bv = v;
+                                delta = RTG_CULL_REL * (omag + tbest * dmag);
+                            }
+                        }
+                    }
+                    if (ANY && occluded) {
+                        cur = RTG_EXIT;
+                    } else if (sp == 0) {
+                        cur = RTG_EXIT;
+                    } else {
+                        --sp;
+                        cur = sp < RTG_STACK ? stk[sp][tid] : io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
+                    }
+                }
+            }
+            if (ANY) {
+                if (io.visible) io.visible[i] = occluded ? 0 : 1;
+                else if (!occluded) io.contrib[pid] = shc;
+            } else {
+                io.hits[i] = make_float4(tbest, __int_as_float(bid), bu, bv);
+            }
+        }
+    }
+    if (COUNT) {
+        // one pair of atomics per wave
+        for (int off = 32; off > 0; off >>= 1) {
+            c_nodes += __shfl_down(c_nodes, off);
+            c_tris += __shfl_down(c_tris, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&io.stats[0], c_nodes);
+            atomicAdd(&io.stats[1], c_tris);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ generate
+__global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
+    const unsigned pid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pid == 0) p.ctr[0].n_ext = a.P;
+    if (pid >= a.P) return;
+    const unsigned lp = pid % a.npix, sl = pid / a.npix;
+    const unsigned pixel = a.pixlist[lp];
+    const unsigned W = (unsigned)a.cam.width;
+    const unsigned x = pixel % W, y = pixel / W;
+    const float px = (float)x + 0.5f, py = (float)y + 0.5f;  // renderTile: pixel centre
+    // Camera::generateRay
+    float xp = px / a.cam.width;
+    float yp = 1.0f - (py / a.cam.height);
+    xp = (xp * 2.0f) - 1.0f;
+    yp = (yp * 2.0f) - 1.0f;
+    const float* m = a.cam.ip;
+    v3 dir = mk(((xp * m[0] + yp * m[1]) + 1.0f * m[2]) + m[3],
+                ((xp * m[4] + yp * m[5]) + 1.0f * m[6]) + m[7],
+                ((xp * m[8] + yp * m[9]) + 1.0f * m[10]) + m[11]);
+    const float* c = a.cam.cm;
+    dir = mk((dir.x * c[0] + dir.y * c[1]) + dir.z * c[2],
+             (dir.x * c[4] + dir.y * c[5]) + dir.z * c[6],
+             (dir.x * c[8] + dir.y * c[9]) + dir.z * c[10]);
+    dir = normalize(dir);
+    ExtRay r;
+    r.o = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, __int_as_float((int)pid));
+    r.d = make_float4(dir.x, dir.y, dir.z, 0.0f);
+    p.q[0][pid] = r;
+    p.thr[pid] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+    p.rng[pid] = pcg_seed(a.seed, pcg_inc(pixel, a.s0 + sl));
+    p.meta[pid] = 1 << 8;  // canHitLight = true
+}
+
+// ------------------------------------------------------------------ shade
+__global__ __launch_bounds__(RTG_TB) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
+    const int lane = lane_id();
+    const unsigned n = p.ctr[b].n_ext;
+    const ExtRay* qin = p.q[b & 1];
+    ExtRay* qout = p.q[(b + 1) & 1];
+    float4* contrib = p.contrib + (size_t)b * a.P;
+    const unsigned wave_global = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const unsigned waves = (gridDim.x * blockDim.x) >> 6;
+    for (unsigned base = wave_global * 64; base < n; base += waves * 64) {
+        const unsigned i = base + lane;
+        bool want_ext = false, want_sh = false;
+        ExtRay next_ray;
+        ShadowRay shr;
+        int pid = 0;
+        if (i < n) {
+            const ExtRay r = qin[i];
+            const float4 h = p.hits[i];
+            pid = __float_as_int(r.o.w);
+            const v3 o = mk(r.o.x, r.o.y, r.o.z), d = mk(r.d.x, r.d.y, r.d.z);
+            const float4 thr4 = p.thr[pid];
+            v3 thr = mk(thr4.x, thr4.y, thr4.z);
+            const int can_hit = (p.meta[pid] >> 8) & 1;
+            const unsigned lp = (unsigned)pid % a.npix, sl = (unsigned)pid / a.npix;
+            const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);
+            uint64_t st = p.rng[pid];
+            v3 c;
+            int nterms = b + 1;
+            if (!(h.x < RTG_FLT_MAX)) {
+                // miss: background->evaluate(r.dir), not weighted by throughput (Renderer.h:390)
+                c = background(s, d);
+            } else {
+                const int tri = __float_as_int(h.y);
+                const float alpha = h.z, beta = h.w, gamma = 1.0f - (alpha + beta);
+                const float t = h.x;
+                const v3 x = add(o, muls(d, t));  // Ray::at
+                const DevShade S = s.shade[tri];
+                const DevMat M = s.mats[__float_as_int(S.d.w)];
+                const v3 n0 = mk(S.a.x, S.a.y, S.a.z), n1 = mk(S.a.w, S.b.x, S.b.y), n2 = mk(S.b.z, S.b.w, S.c.x);
+                v3 sn = normalize(add(add(muls(n0, alpha), muls(n1, beta)), muls(n2, gamma)));
+                const float tu = (S.c.y * alpha + S.c.w * beta) + S.d.y * gamma;
+                const float tv = (S.c.z * alpha + S.d.x * beta) + S.d.z * gamma;
+                const v3 wo = neg(d);
+                if (M.two_sided && dot(wo, sn) < 0) sn = neg(sn);
+                const frame fr = frame_from(sn);
+                if (M.is_light) {
+                    c = can_hit ? mul(thr, mk(M.emission.x, M.emission.y, M.emission.z)) : mk(0.0f, 0.0f, 0.0f);
+                } else {
+                    const bool spec = M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS;
+                    // ---- computeDirect (Renderer.h:423-473)
+                    v3 ld = mk(0.0f, 0.0f, 0.0f);
+                    if (!spec) {
+                        const int nl = s.n_lights;
+                        const float pmf = 1.f / (float)nl;
+                        int li = (int)((float)nl * pcg_next(st, inc));
+                        li = (nl - 1) < li ? (nl - 1) : li;  // (std::min)(a, b)
+                        const DevLight L = s.lights[li];
+                        v3 p2, wi;
+                        float g, pdf;
+                        v3 emitted;
+                        if (__float_as_int(L.v1t.w) == 0) {  // AreaLight::sample -> Triangle::sample
+                            const float r1 = pcg_next(st, inc);
+                            const float r2 = pcg_next(st, inc);
+                            const float la = 1 - sqrtf(r1);
+                            const float lb = r2 * sqrtf(r1);
+                            const float lg = 1.0f - (la + lb);
+                            pdf = 1.0f / L.v0a.w;
+                            p2 = add(add(muls(mk(L.v0a.x, L.v0a.y, L.v0a.z), la), muls(mk(L.v1t.x, L.v1t.y, L.v1t.z), lb)),
+                                     muls(mk(L.v2.x, L.v2.y, L.v2.z), lg));
+                            emitted = mk(L.em.x, L.em.y, L.em.z);
+                            wi = sub(p2, x);
+                            const float l2 = length_sq(wi);
+                            wi = normalize(wi);
+                            g = (wmax(dot(wi, sn), 0.0f) * wmax(-dot(wi, mk(L.gn.x, L.gn.y, L.gn.z)), 0.0f)) / l2;
+                        } else {  // EnvironmentMap::sample: uniformSampleSphere(next(), next())
+                            const float q2 = pcg_next(st, inc);  // evaluated first -> r2
+                            const float q1 = pcg_next(st, inc);  // -> r1
+                            wi = uniform_sample_sphere(q1, q2);
+                            pdf = uniform_sphere_pdf();
+                            emitted = env_eval(s, wi);
+                            g = wmax(dot(wi, sn), 0.0f);
+                            p2 = add(x, muls(wi, 10000.0f));
+                        }
+                        if (g > 0) {
+                            // Scene::visible(x, p2)
+                            v3 sd = sub(p2, x);
+                            const float maxt = sqrtf(length_sq(sd)) - (2.0f * RTG_EPS);
+                            sd = normalize(sd);
+                            const v3 so = add(x, muls(sd, RTG_EPS));
+                            const v3 f = divs(tex_sample(s, M.tex, tu, tv), RTG_PI_F);  // BSDF::evaluate
+                            ld = divs(muls(mul(f, emitted), g), pmf * pdf);
+                            const v3 cvis = mul(thr, ld);
+                            shr.o = make_float4(so.x, so.y, so.z, maxt);
+                            shr.d = make_float4(sd.x, sd.y, sd.z, __int_as_float(pid));
+                            shr.c = make_float4(cvis.x, cvis.y, cvis.z, 0.0f);
+                            want_sh = true;
+                        }
+                    }
+                    // direct = thr * Ld, with Ld = 0 until the shadow ray says visible
+                    c = mul(thr, mk(0.0f, 0.0f, 0.0f));
+                    if (b <= a.max_depth) {
+                        const float rrp = wmin(lum(thr), 0.9f);
+                        if (pcg_next(st, inc) < rrp) {
+                            thr = divs(thr, rrp);
+                            // ---- BSDF::sample
+                            v3 wi, ind;
+                            float pdf;
+                            const v3 alb = tex_sample(s, M.tex, tu, tv);
+                            if (M.kind == RTG_MAT_DIFFUSE || M.kind == RTG_MAT_LAMBERT) {
+                                const float q2 = pcg_next(st, inc);  // cosineSampleHemisphere(next(), next())
+                                const float q1 = pcg_next(st, inc);
+                                const v3 wl = cosine_sample_hemisphere(q1, q2);
+                                if (M.kind == RTG_MAT_DIFFUSE)
+                                    pdf = (wl.z >= 0.0f) ? (float)((double)wl.z / RTM_PI) : 0.0f;
+                                else
+                                    pdf = (float)((double)wl.z / RTM_PI);
+                                ind = divs(alb, RTG_PI_F);
+                                wi = to_world(fr, wl);
+                            } else if (M.kind == RTG_MAT_MIRROR) {
+                                const v3 wol = to_local(fr, wo);
+                                pdf = 1.0f;
+                                ind = alb;
+                                wi = to_world(fr, mk(-wol.x, -wol.y, wol.z));
+                            } else {  // GLASS
+                                const v3 wol = to_local(fr, wo);
+                                const float cos_i = fabsf(wol.z);
+                                const bool enter = wol.z > 0.0f;
+                                const float eta_i = enter ? M.ext_ior : M.int_ior;
+                                const float eta_t = enter ? M.int_ior : M.ext_ior;
+                                v3 wt = mk(0.0f, 0.0f, 0.0f);
+                                const float R = fresnel_dielectric(cos_i, eta_i, eta_t, wt, wol);
+                                if (!enter) wt.z = -wt.z;
+                                const bool refl = (R == 1.0f) || (pcg_next(st, inc) < R);
+                                if (refl) {
+                                    wi = mk(-wol.x, -wol.y, wol.z);
+                                    pdf = R;
+                                    ind = muls(alb, R);
+                                } else {
+                                    wi = wt;
+                                    pdf = 1.0f - R;
+                                    ind = muls(alb, 1.0f - R);
+                                }
+                                wi = to_world(fr, wi);
+                            }
+                            if (spec) thr = divs(mul(thr, ind), pdf);
+                            else thr = divs(muls(mul(thr, ind), fabsf(dot(wi, sn))), pdf);
+                            const v3 no = add(x, muls(wi, RTG_EPS));
+                            next_ray.o = make_float4(no.x, no.y, no.z, __int_as_float(pid));
+                            next_ray.d = make_float4(wi.x, wi.y, wi.z, 0.0f);
+                            want_ext = true;
+                            p.thr[pid] = make_float4(thr.x, thr.y, thr.z, 0.0f);
+                            p.rng[pid] = st;
+                            nterms = (b + 1) | ((spec ? 1 : 0) << 8);
+                        }
+                    }
+                }
+            }
+            contrib[pid] = make_float4(c.x, c.y, c.z, 0.0f);
+            p.meta[pid] = nterms;
+        }
+        // ---- wave-level compaction into the next queues (converged here)
+        const unsigned long long me = __ballot(want_ext);
+        const unsigned long long ms = __ballot(want_sh);
+        unsigned be = 0, bs = 0;
+        if (lane == 0) {
+            if (me) be = atomicAdd(&p.ctr[b + 1].n_ext, (unsigned)__popcll(me));
+            if (ms) bs = atomicAdd(&p.ctr[b].n_shadow, (unsigned)__popcll(ms));
+        }
+        be = __shfl(be, 0);
+        bs = __shfl(bs, 0);
+        if (want_ext) qout[be + prefix_lt(me)] = next_ray;
+        if (want_sh) p.shq[bs + prefix_lt(ms)] = shr;
+    }
+}
+
+// ------------------------------------------------------------------ accumulate
+__global__ __launch_bounds__(RTG_TB) void k_accumulate(ChunkArgs a, PathBufs p, float* film) {
+    const unsigned lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= a.npix) return;
+    const unsigned pixel = a.pixlist[lp];
+    float fr = film[(size_t)pixel * 3 + 0], fg = film[(size_t)pixel * 3 + 1], fb = film[(size_t)pixel * 3 + 2];
+    for (unsigned sl = 0; sl < a.ns; ++sl) {
+        const unsigned pid = sl * a.npix + lp;
+        const int nt = p.meta[pid] & 0xff;
+        float4 acc = p.contrib[(size_t)(nt - 1) * a.P + pid];
+        for (int j = nt - 2; j >= 0; --j) {
+            const float4 c = p.contrib[(size_t)j * a.P + pid];
+            acc = make_float4(c.x + acc.x, c.y + acc.y, c.z + acc.z, 0.0f);
+        }
+        fr = fr + acc.x;
+        fg = fg + acc.y;
+        fb = fb + acc.z;
+    }
+    film[(size_t)pixel * 3 + 0] = fr;
+    film[(size_t)pixel * 3 + 1] = fg;
+    film[(size_t)pixel * 3 + 2] = fb;
+}
+
+// ================================================================== host side (C-ABI)
+static thread_local std::string g_err;
+
+#define HIPOK(expr)                                                                          \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            g_err = std::string(#expr) + ": " + hipGetErrorString(e_);                       \
+            return RTG_ERR_HIP;                                                              \
+        }                                                                                    \
+    } while (0)
+
+template <class T>
+static int dev_upload(T** dst, const std::vector<T>& src) {
+    *dst = nullptr;
+    size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(T);
+    HIPOK(hipMalloc((void**)dst, bytes));
+    if (!src.empty()) HIPOK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return RTG_OK;
+}
+
+struct rtg_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int W = 0, H = 0;
+    uint32_t spp = 0;
+    int max_depth = 4, cull = 1, count = 0, timing = 0;
+    uint32_t max_paths = 1u << 22;
+    int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0, shade_blocks = 0;
+    uint32_t bvh_depth = 0;
+    SceneView sv{};
+    DevCamera cam{};
+    DevNode* d_nodes = nullptr;
+    DevTri* d_tris = nullptr;
+    DevShade* d_shade = nullptr;
+    DevMat* d_mats = nullptr;
+    DevLight* d_lights = nullptr;
+    DevTex* d_texinfo = nullptr;
+    float* d_texels = nullptr;
+    float* d_film = nullptr;
+    // chunk buffers
+    size_t cap_P = 0;
+    int cap_maxb = 0;
+    PathBufs pb{};
+    unsigned* d_pix = nullptr;
+    size_t cap_pix = 0;
+    std::vector<uint32_t> pix_key;
+    unsigned npix = 0;
+    int* d_ovf = nullptr;
+    size_t cap_ovf = 0;
+    unsigned* d_qctr = nullptr;  // query-API counters [4]
+    unsigned long long* d_stats = nullptr;
+    rtg_stats stats{};
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    std::vector<hipEvent_t> kev;  // per-launch timing events (timing mode)
+};
+
+static void free_chunk(rtg_handle* h) {
+    (void)hipFree(h->pb.thr); (void)hipFree(h->pb.rng); (void)hipFree(h->pb.meta); (void)hipFree(h->pb.contrib);
+    (void)hipFree(h->pb.q[0]); (void)hipFree(h->pb.q[1]); (void)hipFree(h->pb.hits); (void)hipFree(h->pb.shq); (void)hipFree(h->pb.ctr);
+    h->pb = PathBufs{};
+    h->cap_P = 0;
+    h->cap_maxb = 0;
+}
+
+static int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
+    if (P <= h->cap_P && maxb <= h->cap_maxb) return RTG_OK;
+    free_chunk(h);
+    PathBufs& p = h->pb;
+    HIPOK(hipMalloc((void**)&p.thr, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.rng, P * sizeof(unsigned long long)));
+    HIPOK(hipMalloc((void**)&p.meta, P * sizeof(int)));
+    HIPOK(hipMalloc((void**)&p.contrib, P * (size_t)maxb * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.q[0], P * sizeof(ExtRay)));
+    HIPOK(hipMalloc((void**)&p.q[1], P * sizeof(ExtRay)));
+    HIPOK(hipMalloc((void**)&p.hits, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.shq, P * sizeof(ShadowRay)));
+    HIPOK(hipMalloc((void**)&p.ctr, (size_t)(maxb + 1) * sizeof(Counters)));
+    h->cap_P = P;
+    h->cap_maxb = maxb;
+    return RTG_OK;
+}
+
+static int ensure_ovf(rtg_handle* h) {
+    int grid = std::max(h->trace_blocks, h->trace_blocks_count);
+    size_t levels = h->bvh_depth + 2 > RTG_STACK ? (size_t)(h->bvh_depth + 2 - RTG_STACK) : 1;
+    size_t need = levels * (size_t)grid * RTG_TB;
+    if (need <= h->cap_ovf) return RTG_OK;
+    (void)hipFree(h->d_ovf);
+    HIPOK(hipMalloc((void**)&h->d_ovf, need * sizeof(int)));
+    h->cap_ovf = need;
+    return RTG_OK;
+}
+
+static float host_bits_f(int v) { float f; std::memcpy(&f, &v, 4); return f; }
+static float host_dot(const float* a, const float* b) { return ((a[0] * b[0]) + (a[1] * b[1])) + (a[2] * b[2]); }
+static void host_cross(const float* a, const float* b, float* o) {
+    o[0] = (a[1] * b[2]) - (a[2] * b[1]);
+    o[1] = (a[2] * b[0]) - (a[0] * b[2]);
+    o[2] = (a[0] * b[1]) - (a[1] * b[0]);
+}
+
+extern "C" {
+
+int32_t rtg_abi_version(void) { return RTG_ABI_VERSION; }
+const char* rtg_last_error(void) { return g_err.c_str(); }
+
+int rtg_device_count(int* count) {
+    if (!count) return RTG_ERR_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return RTG_OK;
+}
+
+static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        g_err = "no HIP device available";
+        return RTG_ERR_NO_DEVICE;
+    }
+    if (device < 0 || device >= ndev) { g_err = "bad device index"; return RTG_ERR_ARG; }
+    if (d->n_lights == 0) {
+        g_err = "scene has no lights (RTBase's Scene::sampleLight indexes an empty list: Scene.h:137-138)";
+        return RTG_ERR_NO_LIGHTS;
+    }
+    h->device = device;
+    HIPOK(hipSetDevice(device));
+    HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    HIPOK(hipGetDeviceProperties(&prop, device));
+    h->n_cu = prop.multiProcessorCount;
+    const uint32_t nt = d->n_tris;
+
+    // ---- triangles: Triangle::init (Geometry.h:72-83) + gNormal (:127-130)
+    std::vector<DevTri> tris(nt);
+    std::vector<DevShade> shade(nt);
+    std::vector<float> tri_area(nt), tri_gn(nt * 3);
+    for (uint32_t i = 0; i < nt; ++i) {
+        const float* P = d->positions + (size_t)i * 9;
+        const float *v0 = P, *v1 = P + 3, *v2 = P + 6;
+        float e1[3] = {v2[0] - v1[0], v2[1] - v1[1], v2[2] - v1[2]};
+        float e2[3] = {v0[0] - v2[0], v0[1] - v2[1], v0[2] - v2[2]};
+        float c[3];
+        host_cross(e1, e2, c);
+        float l = 1.0f / std::sqrt(((c[0] * c[0]) + (c[1] * c[1])) + (c[2] * c[2]));
+        float n[3] = {c[0] * l, c[1] * l, c[2] * l};
+        float dd = host_dot(n, v0);
+        float inv_area = 1.0f / host_dot(c, n);
+        tri_area[i] = std::sqrt(((c[0] * c[0]) + (c[1] * c[1])) + (c[2] * c[2])) * 0.5f;
+        const float* N = d->normals + (size_t)i * 9;
+        float s = host_dot(N, n) > 0 ? 1.0f : -1.0f;
+        for (int k = 0; k < 3; ++k) tri_gn[i * 3 + k] = n[k] * s;
+        tris[i].nd = make_float4(n[0], n[1], n[2], dd);
+        tris[i].v1i = make_float4(v1[0], v1[1], v1[2], inv_area);
+        tris[i].v2 = make_float4(v2[0], v2[1], v2[2], 0.0f);
+        tris[i].e2 = make_float4(e2[0], e2[1], e2[2], 0.0f);
+        const float* U = d->uvs + (size_t)i * 6;
+        if (d->material[i] >= d->n_materials) { g_err = "triangle material index out of range"; return RTG_ERR_ARG; }
+        shade[i].a = make_float4(N[0], N[1], N[2], N[3]);
+        shade[i].b = make_float4(N[4], N[5], N[6], N[7]);
+        shade[i].c = make_float4(N[8], U[0], U[1], U[2]);
+        shade[i].d = make_float4(U[3], U[4], U[5], host_bits_f((int)d->material[i]));
+    }
+    // ---- BVH: reference DFS nodes -> child-pair internal nodes
+    const uint32_t nn = d->n_nodes;
+    if (nn == 0) { g_err = "BVH has no nodes"; return RTG_ERR_ARG; }
+    std::vector<int> internal_id(nn, -1);
+    int n_internal = 0;
+    for (uint32_t i = 0; i < nn; ++i)
+        if (d->node_links[i * 4 + 0] >= 0) internal_id[i] = n_internal++;
+    auto word = [&](int node, int& out) -> bool {
+        const int32_t* L = d->node_links + (size_t)node * 4;
+        if (L[0] >= 0) { out = internal_id[node]; return true; }
+        int cnt = L[3] - L[2];
+        if (cnt < 1 || cnt > 2 || L[2] < 0 || (uint32_t)L[3] > nt) return false;
+        out = ~(L[2] * 2 + (cnt - 1));
+        return true;
+    };
+    std::vector<DevNode> nodes(std::max(n_internal, 1));
+    uint32_t depth = 0;
+    {
+        std::vector<std::pair<int, uint32_t>> st{{0, 0}};
+        while (!st.empty()) {
+            auto [i, dep] = st.back();
+            st.pop_back();
+            depth = std::max(depth, dep);
+            const int32_t* L = d->node_links + (size_t)i * 4;
+            if (L[0] < 0) continue;
+            if (L[0] >= (int)nn || L[1] < 0 || L[1] >= (int)nn) { g_err = "bad BVH link"; return RTG_ERR_ARG; }
+            const float* bl = d->node_bounds + (size_t)L[0] * 6;
+            const float* br = d->node_bounds + (size_t)L[1] * 6;
+            DevNode& dn = nodes[internal_id[i]];
+            dn.a = make_float4(bl[0], bl[1], bl[2], bl[3]);
+            dn.b = make_float4(bl[4], bl[5], br[0], br[1]);
+            dn.c = make_float4(br[2], br[3], br[4], br[5]);
+            int wl, wr;
+            if (!word(L[0], wl) || !word(L[1], wr)) {
+                g_err = "BVH leaf with other than 1-2 triangles (MAXNODE_TRIANGLES = 2)";
+                return RTG_ERR_ARG;
+            }
+            dn.d = make_int4(wl, wr, 0, 0);
+            st.push_back({L[1], dep + 1});
+            st.push_back({L[0], dep + 1});
+        }
+    }
+    h->bvh_depth = depth;
+    int root_word = RTG_EXIT;
+    if (nt > 0) {
+        if (!word(0, root_word)) { g_err = "bad BVH root"; return RTG_ERR_ARG; }
+    }
+    float scale = 0.0f;
+    for (int k = 0; k < 6; ++k) {
+        float v = std::fabs(d->node_bounds[k]);
+        if (std::isfinite(v)) scale = std::max(scale, v);
+    }
+    // ---- materials, textures, lights
+    std::vector<DevMat> mats(d->n_materials);
+    for (uint32_t i = 0; i < d->n_materials; ++i) {
+        const rtg_material& m = d->materials[i];
+        if (m.texture < 0 || (uint32_t)m.texture >= d->n_textures) { g_err = "material texture out of range"; return RTG_ERR_ARG; }
+        mats[i].kind = m.kind;
+        mats[i].two_sided = m.two_sided;
+        mats[i].tex = m.texture;
+        const float lm = ((0.2126f * m.emission[0]) + (0.7152f * m.emission[1])) + (0.0722f * m.emission[2]);
+        mats[i].is_light = lm > 0 ? 1 : 0;
+        mats[i].int_ior = m.int_ior;
+        mats[i].ext_ior = m.ext_ior;
+        mats[i].emission = make_float4(m.emission[0], m.emission[1], m.emission[2], 0.0f);
+    }
+    std::vector<DevTex> texinfo(d->n_textures);
+    std::vector<float> texels;
+    for (uint32_t i = 0; i < d->n_textures; ++i) {
+        const rtg_texture& t = d->textures[i];
+        if (t.width <= 0 || t.height <= 0 || !t.texels) { g_err = "empty texture"; return RTG_ERR_ARG; }
+        texinfo[i] = DevTex{(int)(texels.size() / 3), t.width, t.height, 0};
+        texels.insert(texels.end(), t.texels, t.texels + (size_t)t.width * t.height * 3);
+    }
+    if (d->env_texture >= (int)d->n_textures) { g_err = "env texture out of range"; return RTG_ERR_ARG; }
+    std::vector<DevLight> lights(d->n_lights);
+    for (uint32_t i = 0; i < d->n_lights; ++i) {
+        int li = d->lights[i];
+        DevLight& L = lights[i];
+        std::memset(&L, 0, sizeof(L));
+        if (li < 0) {
+            if (d->env_texture < 0) { g_err = "environment light without an env texture"; return RTG_ERR_ARG; }
+            L.v1t.w = host_bits_f(1);
+            continue;
+        }
+        if ((uint32_t)li >= nt) { g_err = "light triangle out of range"; return RTG_ERR_ARG; }
+        const float* P = d->positions + (size_t)li * 9;
+        const float* em = d->materials[d->material[li]].emission;
+        L.v0a = make_float4(P[0], P[1], P[2], tri_area[li]);
+        L.v1t = make_float4(P[3], P[4], P[5], host_bits_f(0));
+        L.v2 = make_float4(P[6], P[7], P[8], 0.0f);
+        L.gn = make_float4(tri_gn[li * 3], tri_gn[li * 3 + 1], tri_gn[li * 3 + 2], 0.0f);
+        L.em = make_float4(em[0], em[1], em[2], 0.0f);
+    }
+    int rc;
+    if ((rc = dev_upload(&h->d_nodes, nodes))) return rc;
+    if ((rc = dev_upload(&h->d_tris, tris))) return rc;
+    if ((rc = dev_upload(&h->d_shade, shade))) return rc;
+    if ((rc = dev_upload(&h->d_mats, mats))) return rc;
+    if ((rc = dev_upload(&h->d_lights, lights))) return rc;
+    if ((rc = dev_upload(&h->d_texinfo, texinfo))) return rc;
+    if ((rc = dev_upload(&h->d_texels, texels))) return rc;
+
+    SceneView& s = h->sv;
+    s.nodes = h->d_nodes;
+    s.tris = h->d_tris;
+    s.shade = h->d_shade;
+    s.mats = h->d_mats;
+    s.lights = h->d_lights;
+    s.texinfo = h->d_texinfo;
+    s.texels = h->d_texels;
+    s.n_lights = (int)d->n_lights;
+    s.env_tex = d->env_texture;
+    s.root_word = root_word;
+    for (int k = 0; k < 6; ++k) s.root_box[k] = d->node_bounds[k];
+    s.cull_scale = scale;
+
+    std::memcpy(h->cam.ip, d->camera.inv_proj, sizeof(h->cam.ip));
+    std::memcpy(h->cam.cm, d->camera.camera, sizeof(h->cam.cm));
+    h->cam.ox = d->camera.origin[0];
+    h->cam.oy = d->camera.origin[1];
+    h->cam.oz = d->camera.origin[2];
+    h->cam.width = d->camera.width;
+    h->cam.height = d->camera.height;
+    h->W = (int)d->camera.width;
+    h->H = (int)d->camera.height;
+    if (h->W <= 0 || h->H <= 0) { g_err = "bad film size"; return RTG_ERR_ARG; }
+    HIPOK(hipMalloc((void**)&h->d_film, (size_t)h->W * h->H * 3 * sizeof(float)));
+    HIPOK(hipMemset(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float)));
+    HIPOK(hipMalloc((void**)&h->d_qctr, 4 * sizeof(unsigned)));
+    HIPOK(hipMalloc((void**)&h->d_stats, 4 * sizeof(unsigned long long)));
+    HIPOK(hipMemset(h->d_stats, 0, 4 * sizeof(unsigned long long)));
+    for (auto& e : h->ev) HIPOK(hipEventCreate(&e));
+
+    int occ = 0;
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false, false>, RTG_TB, 0));
+    int occ2 = 0;
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_trace<true, false>, RTG_TB, 0));
+    h->trace_blocks = h->n_cu * std::max(1, std::max(occ, occ2));
+    int occ3 = 0, occ4 = 0;
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_trace<false, true>, RTG_TB, 0));
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ4, k_trace<true, true>, RTG_TB, 0));
+    h->trace_blocks_count = h->n_cu * std::max(1, std::max(occ3, occ4));
+    int occs = 0;
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occs, k_shade, RTG_TB, 0));
+    h->shade_blocks = h->n_cu * std::max(1, occs);
+    return ensure_ovf(h);
+}
+
+int rtg_create(int device, const rtg_scene_desc* desc, rtg_handle** out) {
+    if (!desc || !out) { g_err = "rtg_create: null argument"; return RTG_ERR_ARG; }
+    rtg_handle* h = new rtg_handle();
+    int rc = create_impl(device, desc, h);
+    if (rc != RTG_OK) {
+        rtg_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return RTG_OK;
+}
+
+void rtg_destroy(rtg_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    free_chunk(h);
+    (void)hipFree(h->d_nodes); (void)hipFree(h->d_tris); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
+    (void)hipFree(h->d_lights); (void)hipFree(h->d_texinfo); (void)hipFree(h->d_texels); (void)hipFree(h->d_film);
+    (void)hipFree(h->d_pix); (void)hipFree(h->d_ovf); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
+    for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
+    for (auto& e : h->kev) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+int rtg_set_options(rtg_handle* h, int max_depth, int cull, uint32_t max_paths) {
+    if (!h || max_depth < 0 || max_depth > 250) { g_err = "rtg_set_options: bad argument"; return RTG_ERR_ARG; }
+    h->max_depth = max_depth;
+    h->cull = cull & 1;
+    h->count = (cull >> 1) & 1;   // bit 1: counting kernels (node/triangle tests)
+    h->timing = (cull >> 2) & 1;  // bit 2: per-launch timing events
+    if (max_paths) h->max_paths = max_paths;
+    return RTG_OK;
+}
+
+// Pixel list in tile order (32x32 tiles, row-major inside a tile), for the requested tiles.
+static int set_pixels(rtg_handle* h, const uint32_t* tiles, uint32_t n_tiles) {
+    const int TS = 32;
+    const uint32_t tx = (h->W + TS - 1) / TS, ty = (h->H + TS - 1) / TS;
+    std::vector<uint32_t> key;
+    if (tiles) key.assign(tiles, tiles + n_tiles);
+    else key.push_back(0xffffffffu);
+    if (h->d_pix && key == h->pix_key) return RTG_OK;
+    std::vector<uint32_t> pix;
+    auto add_tile = [&](uint32_t t) {
+        uint32_t bx = (t % tx) * TS, by = (t / tx) * TS;
+        for (uint32_t y = by; y < std::min<uint32_t>(by + TS, h->H); ++y)
+            for (uint32_t x = bx; x < std::min<uint32_t>(bx + TS, h->W); ++x) pix.push_back(y * h->W + x);
+    };
+    if (tiles) {
+        for (uint32_t i = 0; i < n_tiles; ++i) {
+            if (tiles[i] >= tx * ty) { g_err = "tile id out of range"; return RTG_ERR_ARG; }
+            add_tile(tiles[i]);
+        }
+    } else {
+        for (uint32_t t = 0; t < tx * ty; ++t) add_tile(t);
+    }
+    if (pix.size() > h->cap_pix) {
+        (void)hipFree(h->d_pix);
+        HIPOK(hipMalloc((void**)&h->d_pix, std::max<size_t>(pix.size(), 1) * 4));
+        h->cap_pix = pix.size();
+    }
+    if (!pix.empty()) HIPOK(hipMemcpy(h->d_pix, pix.data(), pix.size() * 4, hipMemcpyHostToDevice));
+    h->npix = (unsigned)pix.size();
+    h->pix_key = key;
+    return RTG_OK;
+}
+
+static void timed_begin(rtg_handle* h, hipStream_t st, size_t k) {
+    if (!h->timing) return;
+    while (h->kev.size() < 2 * (k + 1)) { hipEvent_t e; (void)hipEventCreate(&e); h->kev.push_back(e); }
+    (void)hipEventRecord(h->kev[2 * k], st);
+}
+static void timed_end(rtg_handle* h, hipStream_t st, size_t k) {
+    if (h->timing) (void)hipEventRecord(h->kev[2 * k + 1], st);
+}
+
+static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed,
+                       const uint32_t* tiles, uint32_t n_tiles, hipStream_t st) {
+    int rc = set_pixels(h, tiles, n_tiles);
+    if (rc) return rc;
+    if (h->npix == 0 || n_samples == 0) return RTG_OK;
+    if ((uint64_t)first + n_samples > 65536u) { g_err = "sample index >= 65536 (PCG stream key)"; return RTG_ERR_ARG; }
+    const int maxb = h->max_depth + 2;
+    uint32_t ns_chunk = std::max<uint32_t>(1, std::min<uint32_t>(n_samples, h->max_paths / std::max(1u, h->npix)));
+    const size_t P = (size_t)ns_chunk * h->npix;
+    if ((rc = ensure_chunk(h, P, maxb))) return rc;
+    if ((rc = ensure_ovf(h))) return rc;
+    HIPOK(hipEventRecord(h->ev[0], st));
+    std::vector<int> kinds;  // 0 extend, 1 shadow, 2 other (timing mode)
+    size_t k = 0;
+    TraceIO io{};
+    io.ovf = h->d_ovf;
+    io.stats = h->d_stats;
+    io.cull = h->cull;
+    for (uint32_t s0 = first; s0 < first + n_samples; s0 += ns_chunk) {
+        ChunkArgs a;
+        a.pixlist = h->d_pix;
+        a.npix = h->npix;
+        a.ns = std::min(ns_chunk, first + n_samples - s0);
+        a.s0 = s0;
+        a.P = a.ns * h->npix;
+        a.seed = seed;
+        a.max_depth = h->max_depth;
+        a.cam = h->cam;
+        HIPOK(hipMemsetAsync(h->pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), st));
+        timed_begin(h, st, k);
+        hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, h->pb);
+        timed_end(h, st, k); kinds.push_back(2); ++k;
+        for (int b = 0; b < maxb; ++b) {
+            io.ext = h->pb.q[b & 1];
+            io.count = &h->pb.ctr[b].n_ext;
+            io.fetch = &h->pb.ctr[b].f_ext;
+            io.hits = h->pb.hits;
+            timed_begin(h, st, k);
+            if (h->count) hipLaunchKernelGGL((k_trace<false, true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
+            else hipLaunchKernelGGL((k_trace<false, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
+            timed_end(h, st, k); kinds.push_back(0); ++k;
+            timed_begin(h, st, k);
+            hipLaunchKernelGGL(k_shade, dim3(h->shade_blocks), dim3(RTG_TB), 0, st, h->sv, a, h->pb, b);
+            timed_end(h, st, k); kinds.push_back(2); ++k;
+            TraceIO sio = io;
+            sio.sh = h->pb.shq;
+            sio.count = &h->pb.ctr[b].n_shadow;
+            sio.fetch = &h->pb.ctr[b].f_shadow;
+            sio.contrib = h->pb.contrib + (size_t)b * a.P;
+            sio.visible = nullptr;
+            timed_begin(h, st, k);
+            if (h->count) hipLaunchKernelGGL((k_trace<true, true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, sio);
+            else hipLaunchKernelGGL((k_trace<true, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, sio);
+            timed_end(h, st, k); kinds.push_back(1); ++k;
+        }
+        timed_begin(h, st, k);
+        hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, h->pb, h->d_film);
+        timed_end(h, st, k); kinds.push_back(2); ++k;
+        HIPOK(hipGetLastError());
+        h->stats.paths += a.P;
+    }
+    HIPOK(hipEventRecord(h->ev[1], st));
+    h->spp += n_samples;
+    if (h->timing) {
+        HIPOK(hipEventSynchronize(h->ev[1]));
+        h->stats.extend_ms = h->stats.shadow_ms = h->stats.shade_ms = 0;
+        for (size_t j = 0; j < kinds.size(); ++j) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, h->kev[2 * j], h->kev[2 * j + 1]);
+            (kinds[j] == 0 ? h->stats.extend_ms : kinds[j] == 1 ? h->stats.shadow_ms : h->stats.shade_ms) += ms;
+        }
+    }
+    return RTG_OK;
+}
+
+int rtg_render_async(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, const uint32_t* tiles,
+                     uint32_t n_tiles, void* stream) {
+    if (!h) { g_err = "null handle"; return RTG_ERR_ARG; }
+    HIPOK(hipSetDevice(h->device));
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    return render_impl(h, first, n, seed, tiles, n_tiles, st);
+}
+
+int rtg_render(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, const uint32_t* tiles, uint32_t n_tiles) {
+    int rc = rtg_render_async(h, first, n, seed, tiles, n_tiles, nullptr);
+    if (rc) return rc;
+    return rtg_synchronize(h);
+}
+
+int rtg_synchronize(rtg_handle* h) {
+    if (!h) return RTG_ERR_ARG;
+    HIPOK(hipStreamSynchronize(h->stream));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, h->ev[0], h->ev[1]) == hipSuccess) h->stats.render_ms = ms;
+    return RTG_OK;
+}
+
+int rtg_film_read(rtg_handle* h, float* rgb, uint32_t* spp) {
+    if (!h) return RTG_ERR_ARG;
+    HIPOK(hipSetDevice(h->device));
+    HIPOK(hipStreamSynchronize(h->stream));
+    if (rgb) HIPOK(hipMemcpy(rgb, h->d_film, (size_t)h->W * h->H * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    if (spp) *spp = h->spp;
+    return RTG_OK;
+}
+
+int rtg_film_copy_device(rtg_handle* h, void* dst) {
+    if (!h || !dst) return RTG_ERR_ARG;
+    HIPOK(hipSetDevice(h->device));
+    HIPOK(hipMemcpyAsync(dst, h->d_film, (size_t)h->W * h->H * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
+    HIPOK(hipStreamSynchronize(h->stream));
+    return RTG_OK;
+}
+
+int rtg_film_load(rtg_handle* h, const float* rgb, uint32_t spp) {
+    if (!h || !rgb) return RTG_ERR_ARG;
+    HIPOK(hipSetDevice(h->device));
+    HIPOK(hipMemcpy(h->d_film, rgb, (size_t)h->W * h->H * 3 * sizeof(float), hipMemcpyHostToDevice));
+    h->spp = spp;
+    return RTG_OK;
+}
+
+int rtg_clear(rtg_handle* h) {
+    if (!h) return RTG_ERR_ARG;
+    HIPOK(hipSetDevice(h->device));
+    HIPOK(hipMemsetAsync(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float), h->stream));
+    HIPOK(hipStreamSynchronize(h->stream));
+    h->spp = 0;
+    return RTG_OK;
+}
+
+int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
+    if (!h || !out) return RTG_ERR_ARG;
+    HIPOK(hipSetDevice(h->device));
+    HIPOK(hipStreamSynchronize(h->stream));
+    unsigned long long c[4] = {0, 0, 0, 0};
+    HIPOK(hipMemcpy(c, h->d_stats, sizeof(c), hipMemcpyDeviceToHost));
+    h->stats.node_visits = c[0];
+    h->stats.tri_tests = c[1];
+    *out = h->stats;
+    return RTG_OK;
+}
+
+static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits, int32_t* vis, bool any) {
+    if (!h || !rays || (!hits && !vis)) return RTG_ERR_ARG;
+    if (n == 0) return RTG_OK;
+    HIPOK(hipSetDevice(h->device));
+    void* d_in = nullptr;
+    void* d_out = nullptr;
+    size_t in_bytes = (size_t)n * (any ? sizeof(ShadowRay) : sizeof(ExtRay));
+    HIPOK(hipMalloc(&d_in, in_bytes));
+    HIPOK(hipMalloc(&d_out, (size_t)n * (any ? sizeof(int) : sizeof(float4))));
+    if (any) {
+        std::vector<ShadowRay> v(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            const float* r = rays + (size_t)i * 8;
+            v[i].o = make_float4(r[0], r[1], r[2], r[3]);
+            v[i].d = make_float4(r[4], r[5], r[6], host_bits_f(0));
+            v[i].c = make_float4(0, 0, 0, 0);
+        }
+        HIPOK(hipMemcpy(d_in, v.data(), in_bytes, hipMemcpyHostToDevice));
+    } else {
+        std::vector<ExtRay> v(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            const float* r = rays + (size_t)i * 8;
+            v[i].o = make_float4(r[0], r[1], r[2], 0.0f);
+            v[i].d = make_float4(r[4], r[5], r[6], 0.0f);
+        }
+        HIPOK(hipMemcpy(d_in, v.data(), in_bytes, hipMemcpyHostToDevice));
+    }
+    unsigned hc[4] = {n, 0, 0, 0};
+    HIPOK(hipMemcpy(h->d_qctr, hc, sizeof(hc), hipMemcpyHostToDevice));
+    int rc = ensure_ovf(h);
+    if (rc) return rc;
+    TraceIO io{};
+    io.count = h->d_qctr;
+    io.fetch = h->d_qctr + 1;
+    io.ovf = h->d_ovf;
+    io.stats = h->d_stats;
+    io.cull = h->cull;
+    if (any) {
+        io.sh = (const ShadowRay*)d_in;
+        io.visible = (int*)d_out;
+        hipLaunchKernelGGL((k_trace<true, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, io);
+    } else {
+        io.ext = (const ExtRay*)d_in;
+        io.hits = (float4*)d_out;
+        hipLaunchKernelGGL((k_trace<false, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, io);
+    }
+    HIPOK(hipGetLastError());
+    HIPOK(hipStreamSynchronize(h->stream));
+    if (any) HIPOK(hipMemcpy(vis, d_out, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
+    else HIPOK(hipMemcpy(hits, d_out, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return RTG_OK;
+}
+
+int rtg_trace_closest(rtg_handle* h, const float* rays, uint32_t n, float* hits) {
+    return trace_query(h, rays, n, hits, nullptr, false);
+}
+int rtg_trace_visible(rtg_handle* h, const float* rays, uint32_t n, int32_t* visible) {
+    return trace_query(h, rays, n, nullptr, visible, true);
+}
+
+}  // extern "C"

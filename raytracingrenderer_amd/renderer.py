@@ -1,0 +1,227 @@
+"""Python mirror of RTBase's host-facing API on top of the native libraries.
+
+  loadScene(name, ...)          -> Scene         RTBase/SceneLoader.h:237-291 (librth)
+  RayTracer(scene, device)      .init/.render/.getSPP/.clear/.saveHDR   RTBase/Renderer.h:45-898
+  Scene.triangles/.lights       post-BVH-build arrays (numpy views of the flattened Scene)
+
+RayTracer.render() is the drop-in for RayTracer::render(): it adds one sample per pixel through
+the HIP wavefront path tracer (librtg). There is no CPU fallback; without a GPU, RayTracer raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _native as N
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _check(rc, lib_err):
+    if rc != 0:
+        raise NativeError("%s (code %d)" % (lib_err().decode(errors="replace"), rc))
+
+
+class Scene:
+    """The flattened reference Scene produced by the host front-end (rth_load_scene)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        self.desc_ptr = N.rth().rth_scene_desc(handle)
+        self.desc = self.desc_ptr.contents
+        info = N.rth_scene_info()
+        _check(N.rth().rth_scene_get_info(handle, C.byref(info)), N.rth().rth_last_error)
+        self.info = info
+        self.width, self.height = info.width, info.height
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            N.rth().rth_free_scene(h)
+
+    # numpy views (no copy) of the flattened arrays
+    def _view(self, p, n, dtype):
+        if n == 0:
+            return np.zeros(0, dtype)
+        return np.ctypeslib.as_array(p, shape=(n,)).view(dtype)
+
+    @property
+    def positions(self):
+        return self._view(self.desc.positions, self.desc.n_tris * 9, np.float32).reshape(-1, 3, 3)
+
+    @property
+    def normals(self):
+        return self._view(self.desc.normals, self.desc.n_tris * 9, np.float32).reshape(-1, 3, 3)
+
+    @property
+    def uvs(self):
+        return self._view(self.desc.uvs, self.desc.n_tris * 6, np.float32).reshape(-1, 3, 2)
+
+    @property
+    def material_index(self):
+        return self._view(self.desc.material, self.desc.n_tris, np.uint32)
+
+    @property
+    def node_bounds(self):
+        return self._view(self.desc.node_bounds, self.desc.n_nodes * 6, np.float32).reshape(-1, 6)
+
+    @property
+    def node_links(self):
+        return self._view(self.desc.node_links, self.desc.n_nodes * 4, np.int32).reshape(-1, 4)
+
+    @property
+    def lights(self):
+        return self._view(self.desc.lights, self.desc.n_lights, np.int32)
+
+    @property
+    def materials(self):
+        return [self.desc.materials[i] for i in range(self.desc.n_materials)]
+
+    def texture(self, i):
+        t = self.desc.textures[i]
+        return self._view(t.texels, t.width * t.height * 3, np.float32).reshape(t.height, t.width, 3)
+
+    @property
+    def camera(self):
+        c = self.desc.camera
+        return {"inv_proj": np.array(c.inv_proj[:], np.float32).reshape(4, 4),
+                "camera": np.array(c.camera[:], np.float32).reshape(4, 4),
+                "origin": np.array(c.origin[:], np.float32), "width": c.width, "height": c.height}
+
+    def permutation(self):
+        out = np.zeros(self.desc.n_tris, np.uint32)
+        _check(N.rth().rth_scene_permutation(self._h, N.ptr(out, C.c_uint32)), N.rth().rth_last_error)
+        return out
+
+
+def loadScene(scene_dir, width=0, height=0, skip_missing=False, envmap=None, bvh_threads=0):
+    """RTBase loadScene(sceneName) with optional film-size / env overrides (applied before P)."""
+    opts = N.rth_load_options(int(width), int(height), 1 if skip_missing else 0, int(bvh_threads),
+                              envmap.encode() if envmap else None)
+    h = C.c_void_p()
+    _check(N.rth().rth_load_scene(os.fsencode(scene_dir), C.byref(opts), C.byref(h)), N.rth().rth_last_error)
+    return Scene(h)
+
+
+def write_synthetic_scene(out_dir, n_tris=1_000_000, seed=20251015, width=1024, height=1024):
+    """C3 synthetic scene as .gem + scene.json + albedo.png + env.hdr."""
+    os.makedirs(out_dir, exist_ok=True)
+    _check(N.rth().rth_write_synthetic(os.fsencode(out_dir), n_tris, seed, width, height), N.rth().rth_last_error)
+    return out_dir
+
+
+def save_hdr(path, film_sum, spp):
+    """Film::save: film / SPP -> RLE RGBE (stbi_write_hdr format)."""
+    f = np.ascontiguousarray(film_sum, np.float32)
+    h, w = f.shape[0], f.shape[1]
+    _check(N.rth().rth_save_hdr(os.fsencode(path), w, h, N.ptr(f, C.c_float), spp), N.rth().rth_last_error)
+
+
+def read_hdr(path):
+    w, h = C.c_int32(), C.c_int32()
+    p = N.f32p()
+    _check(N.rth().rth_read_hdr(os.fsencode(path), C.byref(w), C.byref(h), C.byref(p)), N.rth().rth_last_error)
+    try:
+        return np.ctypeslib.as_array(p, shape=(h.value, w.value, 3)).copy()
+    finally:
+        N.rth().rth_free(C.cast(p, C.c_void_p))
+
+
+class RayTracer:
+    """RayTracer (Renderer.h:31-899) backed by librtg on one GPU."""
+
+    MAX_DEPTH = 4  # Renderer.h:20
+
+    def __init__(self, scene, device=0, max_depth=MAX_DEPTH, seed=1234, cull=True, max_paths=0):
+        self.scene = scene
+        self.seed = seed
+        self._lib = N.rtg()
+        h = C.c_void_p()
+        _check(self._lib.rtg_create(device, scene.desc_ptr, C.byref(h)), self._lib.rtg_last_error)
+        self._h = h
+        self.width, self.height = scene.width, scene.height
+        self.max_depth = max_depth
+        self.flags = N.RTG_OPT_CULL if cull else 0
+        self.set_options(max_depth=max_depth, flags=self.flags, max_paths=max_paths)
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.rtg_destroy(h)
+
+    def set_options(self, max_depth=None, flags=None, max_paths=0):
+        if max_depth is not None:
+            self.max_depth = max_depth
+        if flags is not None:
+            self.flags = flags
+        _check(self._lib.rtg_set_options(self._h, self.max_depth, self.flags, max_paths), self._lib.rtg_last_error)
+
+    @property
+    def tiles_x(self):
+        return (self.width + 31) // 32
+
+    @property
+    def tiles_y(self):
+        return (self.height + 31) // 32
+
+    def render(self, n_samples=1, tiles=None, first_sample=None, sync=True):
+        """RayTracer::render(): add n_samples samples per pixel (default 1 = one frame)."""
+        first = self.getSPP() if first_sample is None else first_sample
+        t = None if tiles is None else np.ascontiguousarray(tiles, np.uint32)
+        tp = N.ptr(t, C.c_uint32) if t is not None else None
+        nt = 0 if t is None else len(t)
+        if sync:
+            rc = self._lib.rtg_render(self._h, first, n_samples, self.seed, tp, nt)
+        else:
+            rc = self._lib.rtg_render_async(self._h, first, n_samples, self.seed, tp, nt, None)
+        _check(rc, self._lib.rtg_last_error)
+
+    def synchronize(self):
+        _check(self._lib.rtg_synchronize(self._h), self._lib.rtg_last_error)
+
+    def film(self):
+        """(sum, spp): the unnormalised Film::film and Film::SPP."""
+        out = np.zeros((self.height, self.width, 3), np.float32)
+        spp = C.c_uint32()
+        _check(self._lib.rtg_film_read(self._h, N.ptr(out, C.c_float), C.byref(spp)), self._lib.rtg_last_error)
+        return out, spp.value
+
+    def load_film(self, film_sum, spp):
+        f = np.ascontiguousarray(film_sum, np.float32)
+        _check(self._lib.rtg_film_load(self._h, N.ptr(f, C.c_float), spp), self._lib.rtg_last_error)
+
+    def copy_film_to(self, device_ptr):
+        _check(self._lib.rtg_film_copy_device(self._h, C.c_void_p(device_ptr)), self._lib.rtg_last_error)
+
+    def getSPP(self):
+        spp = C.c_uint32()
+        _check(self._lib.rtg_film_read(self._h, None, C.byref(spp)), self._lib.rtg_last_error)
+        return spp.value
+
+    def clear(self):
+        _check(self._lib.rtg_clear(self._h), self._lib.rtg_last_error)
+
+    def saveHDR(self, filename):
+        f, spp = self.film()
+        save_hdr(filename, f, max(spp, 1))
+
+    def stats(self):
+        s = N.rtg_stats()
+        _check(self._lib.rtg_get_stats(self._h, C.byref(s)), self._lib.rtg_last_error)
+        return {k: getattr(s, k) for k, _ in N.rtg_stats._fields_}
+
+    def trace_closest(self, rays):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        out = np.zeros((len(r), 4), np.float32)
+        _check(self._lib.rtg_trace_closest(self._h, N.ptr(r, C.c_float), len(r), N.ptr(out, C.c_float)),
+               self._lib.rtg_last_error)
+        return out
+
+    def trace_visible(self, rays):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        out = np.zeros(len(r), np.int32)
+        _check(self._lib.rtg_trace_visible(self._h, N.ptr(r, C.c_float), len(r), N.ptr(out, C.c_int32)),
+               self._lib.rtg_last_error)
+        return out
