@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Headline benchmark: BASELINE.json metric "Mray/s + ms/frame at 1024x1024x64spp; achieved HBM GB/s
+vs peak" on config C3 (synthetic 1M random triangles, 1024x1024, 64 spp, MAX_DEPTH 4).
+
+One step = one complete 1024x1024x64spp render (64 RayTracer::render() frames) of this rank's
+32x32 tiles (tile_id % world_size == rank) through the HIP wavefront tracer, plus, for N > 1, the
+RCCL reduce(sum) of the float32 radiance film to rank 0 over xGMI (tile supports are disjoint, so
+the reduced film is bit-identical to a 1-GPU render). Total work is fixed as N grows (strong
+scaling). Scene generation, loading and BVH build happen before the timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--width", type=int, default=1024)
+    p.add_argument("--height", type=int, default=1024)
+    p.add_argument("--spp", type=int, default=64)
+    p.add_argument("--max-depth", type=int, default=4)
+    p.add_argument("--tris", type=int, default=1_000_000)
+    p.add_argument("--seed", type=int, default=20251015)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--max-paths", type=int, default=0, help="paths per wavefront chunk (0 = library default)")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from raytracingrenderer_amd import RayTracer, loadScene, write_synthetic_scene
+    from raytracingrenderer_amd import _native as N
+
+    # ---- scene (outside the timed region)
+    work = tempfile.mkdtemp(prefix="rtg_bench_r%d_" % rank)
+    t0 = time.time()
+    write_synthetic_scene(work, n_tris=a.tris, seed=a.seed, width=a.width, height=a.height)
+    scene = loadScene(work)
+    setup_s = time.time() - t0
+    rt = RayTracer(scene, device=local, max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
+    tiles_all = np.arange(rt.tiles_x * rt.tiles_y, dtype=np.uint32)
+    tiles = tiles_all[tiles_all % world == rank]
+
+    film_t = None
+    if world > 1:
+        import torch
+        film_t = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device="cuda:%d" % local)
+
+    def step():
+        rt.clear()
+        rt.render(a.spp, tiles=tiles, first_sample=0)
+        if world > 1:
+            rt.copy_film_to(film_t.data_ptr())
+            dist.reduce(film_t, dst=0, op=dist.ReduceOp.SUM)
+
+    def barrier_sync():
+        if world > 1:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+        else:
+            rt.synchronize()
+
+    for _ in range(a.warmup):
+        step()
+    # timed region: per-launch HIP events on the render stream give the closest-hit kernel time
+    rt.set_options(flags=N.RTG_OPT_CULL | N.RTG_OPT_TIMING)
+    ext_rays = shadow_rays = paths = 0
+    extend_ms = 0.0
+    extend_launches = 0
+    barrier_sync()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+        st = rt.stats()
+        ext_rays += st["extension_rays"]
+        shadow_rays += st["shadow_rays"]
+        paths += st["paths"]
+        extend_ms += st["extend_ms"]
+        extend_launches += st["extend_launches"]
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
+    rt.set_options(flags=N.RTG_OPT_CULL)
+
+    # counting pass (untimed): box / triangle tests per closest-hit ray on the same workload
+    rt.set_options(flags=N.RTG_OPT_CULL | N.RTG_OPT_COUNT)
+    rt.clear()
+    rt.render(a.spp, tiles=tiles, first_sample=0)
+    cs = rt.stats()
+    rt.set_options(flags=N.RTG_OPT_CULL)
+
+    totals = np.array([ext_rays, shadow_rays, paths, extend_ms, extend_launches,
+                       cs["node_visits"], cs["tri_tests"], cs["extension_rays"]], dtype=np.float64)
+    t_max = elapsed
+    if world > 1:
+        import torch
+        tt = torch.tensor(totals, dtype=torch.float64, device="cuda:%d" % local)
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        totals = tt.cpu().numpy()
+        te = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        t_max = float(te.item())
+    ext_rays, shadow_rays, paths, extend_ms, extend_launches, c_nodes, c_tris, c_ext = totals.tolist()
+    rays = ext_rays + shadow_rays
+    mrays = rays / t_max / 1e6
+    ms_step = t_max * 1e3 / a.steps
+
+    # roofline for the dominant kernel (closest-hit traversal): algorithmic bytes per ray
+    # B = 32 B x box tests + 36 B x triangle tests + 48 B ray I/O
+    boxes_per_ray = c_nodes / max(c_ext, 1)
+    tris_per_ray = c_tris / max(c_ext, 1)
+    b_ray = 32.0 * boxes_per_ray + 36.0 * tris_per_ray + 48.0
+    # per-rank average launch: ext rays and time both summed over ranks/launches
+    achieved_gbs = (b_ray * ext_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
+    traffic = None
+    if os.path.exists(PMC_SUMMARY):
+        try:
+            traffic = json.load(open(PMC_SUMMARY)).get("extend_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(scene, a)
+
+    if rank == 0:
+        out = {
+            "metric": "Mray/s (closest-hit + shadow rays) at 1024x1024x64spp, synthetic 1M triangles",
+            "value": round(mrays, 2),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "ms_per_frame": round(ms_step / a.spp, 4),
+            "mpaths_per_s": round(paths / t_max / 1e6, 2),
+            "rays_per_path": round(rays / max(paths, 1), 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (splitmix64 random triangles, generated in-run)",
+            "config": {"workload": "C3: synth-1M, %dx%d, %d spp, MAX_DEPTH %d" % (a.width, a.height, a.spp, a.max_depth),
+                       "triangles": a.tris, "width": a.width, "height": a.height, "spp": a.spp,
+                       "max_depth": a.max_depth, "parallelism": "tile-sharded x%d + RCCL film reduce" % world},
+            "roofline": {"bound": "hbm", "kernel": "k_trace<closest>",
+                         "achieved": None if achieved_gbs is None else round(achieved_gbs, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": None if achieved_gbs is None else round(achieved_gbs / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
+                         "tri_tests_per_ray": round(tris_per_ray, 2),
+                         "avg_launch_ms": round(extend_ms / max(extend_launches, 1), 4)},
+            "cpu_baseline": cpu,
+            "setup_s": round(setup_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(scene, a):
+    """The C oracle's tile renderer (the reference algorithm: unordered DFS, no culling) on the
+    host cores, bounded sample: whole 1-spp frames of the same scene until ~cpu_seconds pass."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        from oracle.pyoracle import Oracle
+    except Exception as e:  # pragma: no cover
+        return {"error": "oracle unavailable: %s" % e}
+    threads = min(16, os.cpu_count() or 1)
+    o = Oracle(scene, max_depth=a.max_depth, flavour="libm")
+    rays = paths = 0
+    frames = 0
+    t0 = time.perf_counter()
+    film = np.zeros((scene.height, scene.width, 3), np.float32)
+    while frames < 8:
+        _, c = o.render(1, first=frames, seed=1234, threads=threads, film=film, count=True)
+        paths += int(c[0])
+        rays += int(c[1] + c[2])
+        frames += 1
+        if time.perf_counter() - t0 > a.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
+            "sample": "%d full %dx%d frame(s) at 1 spp of the same synth-1M scene (%d paths, %d rays) in %.1f s; "
+                      "oracle/rt_oracle.c tile renderer (reference DFS traversal, no culling), %d threads"
+                      % (frames, scene.width, scene.height, paths, rays, dt, threads),
+            "ms_per_frame": round(dt * 1e3 / frames, 1)}
+
+
+if __name__ == "__main__":
+    main()

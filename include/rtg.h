@@ -91,10 +91,13 @@ typedef struct rtg_stats {
     uint64_t paths;                /* camera paths traced                                      */
     uint64_t extension_rays;       /* closest-hit queries (Scene::traverse)                    */
     uint64_t shadow_rays;          /* any-hit queries (Scene::visible)                         */
-    uint64_t node_visits;          /* counting builds only (0 otherwise)                       */
-    uint64_t tri_tests;            /* counting builds only (0 otherwise)                       */
+    uint64_t node_visits;          /* RTG_OPT_COUNT: box tests by closest-hit rays             */
+    uint64_t tri_tests;            /* RTG_OPT_COUNT: triangle tests by closest-hit rays        */
+    uint64_t shadow_node_visits;   /* RTG_OPT_COUNT: box tests by any-hit rays                 */
+    uint64_t shadow_tri_tests;     /* RTG_OPT_COUNT: triangle tests by any-hit rays            */
+    uint64_t extend_launches;      /* RTG_OPT_TIMING: closest-hit launches in the last call    */
     double   render_ms;            /* device time of the last rtg_render call                  */
-    double   extend_ms;            /* device time spent in closest-hit kernels (last call)     */
+    double   extend_ms;            /* RTG_OPT_TIMING: closest-hit kernel time (last call)      */
     double   shadow_ms;            /* device time spent in any-hit kernels (last call)         */
     double   shade_ms;             /* device time spent in generate/shade/accumulate kernels   */
 } rtg_stats;
@@ -114,7 +117,7 @@ void rtg_destroy(rtg_handle* h);
  * culling (without it traversal visits exactly the reference's node set: verification mode);
  * RTG_OPT_COUNT runs the counting kernels (node / triangle tests in rtg_stats);
  * RTG_OPT_TIMING records HIP events around every launch (per-kernel-class ms in rtg_stats).
- * max_paths_in_flight bounds the paths of one wavefront chunk (0 = keep, default 4M). */
+ * max_paths_in_flight bounds the paths of one wavefront chunk (0 = keep, default 64M). */
 #define RTG_OPT_CULL   1
 #define RTG_OPT_COUNT  2
 #define RTG_OPT_TIMING 4

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -50,7 +51,7 @@ struct TraceIO {
     float4* contrib;           // any-hit: write ShadowRay.c to contrib[pid] when visible
     int* visible;              // any-hit query output (instead of contrib)
     int* ovf;                  // global stack overflow [level][thread]
-    unsigned long long* stats; // [0] node visits, [1] triangle tests (COUNT builds)
+    unsigned long long* stats; // [0,1] closest / [4,5] any-hit: box tests, triangle tests (COUNT)
     int cull;
 };
 
@@ -198,8 +199,8 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
             c_tris += __shfl_down(c_tris, off);
         }
         if (lane == 0) {
-            atomicAdd(&io.stats[0], c_nodes);
-            atomicAdd(&io.stats[1], c_tris);
+            atomicAdd(&io.stats[ANY ? 4 : 0], c_nodes);
+            atomicAdd(&io.stats[ANY ? 5 : 1], c_tris);
         }
     }
 }
@@ -435,6 +436,18 @@ __global__ __launch_bounds__(RTG_TB) void k_accumulate(ChunkArgs a, PathBufs p, 
     film[(size_t)pixel * 3 + 2] = fb;
 }
 
+// Per-chunk ray tally: extension + shadow queue lengths of every bounce into stats[2..3].
+__global__ void k_tally(const Counters* ctr, int maxb, unsigned long long* stats) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    unsigned long long e = 0, sh = 0;
+    for (int b = 0; b < maxb; ++b) {
+        e += ctr[b].n_ext;
+        sh += ctr[b].n_shadow;
+    }
+    stats[2] += e;
+    stats[3] += sh;
+}
+
 // ================================================================== host side (C-ABI)
 static thread_local std::string g_err;
 
@@ -462,7 +475,7 @@ struct rtg_handle {
     int W = 0, H = 0;
     uint32_t spp = 0;
     int max_depth = 4, cull = 1, count = 0, timing = 0;
-    uint32_t max_paths = 1u << 22;
+    uint32_t max_paths = 1u << 26;  // 64M paths in flight (~17 GB at depth 4 of 288 GB HBM)
     int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0, shade_blocks = 0;
     uint32_t bvh_depth = 0;
     SceneView sv{};
@@ -563,7 +576,8 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     }
     h->device = device;
     HIPOK(hipSetDevice(device));
-    HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    if (std::getenv("RTG_NULL_STREAM")) h->stream = nullptr;  // legacy default stream (profiling aid)
+    else HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     HIPOK(hipGetDeviceProperties(&prop, device));
     h->n_cu = prop.multiProcessorCount;
@@ -729,8 +743,8 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     HIPOK(hipMalloc((void**)&h->d_film, (size_t)h->W * h->H * 3 * sizeof(float)));
     HIPOK(hipMemset(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float)));
     HIPOK(hipMalloc((void**)&h->d_qctr, 4 * sizeof(unsigned)));
-    HIPOK(hipMalloc((void**)&h->d_stats, 4 * sizeof(unsigned long long)));
-    HIPOK(hipMemset(h->d_stats, 0, 4 * sizeof(unsigned long long)));
+    HIPOK(hipMalloc((void**)&h->d_stats, 8 * sizeof(unsigned long long)));
+    HIPOK(hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)));
     for (auto& e : h->ev) HIPOK(hipEventCreate(&e));
 
     int occ = 0;
@@ -817,6 +831,15 @@ static int set_pixels(rtg_handle* h, const uint32_t* tiles, uint32_t n_tiles) {
     return RTG_OK;
 }
 
+#define LAUNCH_OK(name)                                                                      \
+    do {                                                                                     \
+        hipError_t e_ = hipGetLastError();                                                   \
+        if (e_ != hipSuccess) {                                                              \
+            g_err = std::string("launch ") + name + ": " + hipGetErrorString(e_);            \
+            return RTG_ERR_HIP;                                                              \
+        }                                                                                    \
+    } while (0)
+
 static void timed_begin(rtg_handle* h, hipStream_t st, size_t k) {
     if (!h->timing) return;
     while (h->kev.size() < 2 * (k + 1)) { hipEvent_t e; (void)hipEventCreate(&e); h->kev.push_back(e); }
@@ -837,6 +860,7 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
     const size_t P = (size_t)ns_chunk * h->npix;
     if ((rc = ensure_chunk(h, P, maxb))) return rc;
     if ((rc = ensure_ovf(h))) return rc;
+    (void)hipGetLastError();  // drop any stale error left by other code on this thread
     HIPOK(hipEventRecord(h->ev[0], st));
     std::vector<int> kinds;  // 0 extend, 1 shadow, 2 other (timing mode)
     size_t k = 0;
@@ -857,6 +881,7 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
         HIPOK(hipMemsetAsync(h->pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), st));
         timed_begin(h, st, k);
         hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, h->pb);
+        LAUNCH_OK("k_generate");
         timed_end(h, st, k); kinds.push_back(2); ++k;
         for (int b = 0; b < maxb; ++b) {
             io.ext = h->pb.q[b & 1];
@@ -866,9 +891,11 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
             timed_begin(h, st, k);
             if (h->count) hipLaunchKernelGGL((k_trace<false, true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
             else hipLaunchKernelGGL((k_trace<false, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
+            LAUNCH_OK("k_trace<closest>");
             timed_end(h, st, k); kinds.push_back(0); ++k;
             timed_begin(h, st, k);
             hipLaunchKernelGGL(k_shade, dim3(h->shade_blocks), dim3(RTG_TB), 0, st, h->sv, a, h->pb, b);
+            LAUNCH_OK("k_shade");
             timed_end(h, st, k); kinds.push_back(2); ++k;
             TraceIO sio = io;
             sio.sh = h->pb.shq;
@@ -879,12 +906,15 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
             timed_begin(h, st, k);
             if (h->count) hipLaunchKernelGGL((k_trace<true, true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, sio);
             else hipLaunchKernelGGL((k_trace<true, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, sio);
+            LAUNCH_OK("k_trace<any>");
             timed_end(h, st, k); kinds.push_back(1); ++k;
         }
+        hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, st, h->pb.ctr, maxb, h->d_stats);
+        LAUNCH_OK("k_tally");
         timed_begin(h, st, k);
         hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, h->pb, h->d_film);
+        LAUNCH_OK("k_accumulate");
         timed_end(h, st, k); kinds.push_back(2); ++k;
-        HIPOK(hipGetLastError());
         h->stats.paths += a.P;
     }
     HIPOK(hipEventRecord(h->ev[1], st));
@@ -892,10 +922,12 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
     if (h->timing) {
         HIPOK(hipEventSynchronize(h->ev[1]));
         h->stats.extend_ms = h->stats.shadow_ms = h->stats.shade_ms = 0;
+        h->stats.extend_launches = 0;
         for (size_t j = 0; j < kinds.size(); ++j) {
             float ms = 0;
             (void)hipEventElapsedTime(&ms, h->kev[2 * j], h->kev[2 * j + 1]);
             (kinds[j] == 0 ? h->stats.extend_ms : kinds[j] == 1 ? h->stats.shadow_ms : h->stats.shade_ms) += ms;
+            if (kinds[j] == 0) h->stats.extend_launches++;
         }
     }
     return RTG_OK;
@@ -952,8 +984,10 @@ int rtg_clear(rtg_handle* h) {
     if (!h) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
     HIPOK(hipMemsetAsync(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float), h->stream));
+    HIPOK(hipMemsetAsync(h->d_stats, 0, 8 * sizeof(unsigned long long), h->stream));
     HIPOK(hipStreamSynchronize(h->stream));
     h->spp = 0;
+    h->stats = rtg_stats{};
     return RTG_OK;
 }
 
@@ -961,10 +995,14 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     if (!h || !out) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
     HIPOK(hipStreamSynchronize(h->stream));
-    unsigned long long c[4] = {0, 0, 0, 0};
+    unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPOK(hipMemcpy(c, h->d_stats, sizeof(c), hipMemcpyDeviceToHost));
     h->stats.node_visits = c[0];
     h->stats.tri_tests = c[1];
+    h->stats.extension_rays = c[2];
+    h->stats.shadow_rays = c[3];
+    h->stats.shadow_node_visits = c[4];
+    h->stats.shadow_tri_tests = c[5];
     *out = h->stats;
     return RTG_OK;
 }
