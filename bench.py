@@ -66,8 +66,8 @@ def main():
     scene = loadScene(work)
     setup_s = time.time() - t0
     rt = RayTracer(scene, device=local, max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
-    tiles_all = np.arange(rt.tiles_x * rt.tiles_y, dtype=np.uint32)
-    tiles = tiles_all[tiles_all % world == rank]
+    from raytracingrenderer_amd.distributed import reduce_film, tiles_for_rank
+    tiles = tiles_for_rank(a.width, a.height, rank, world)
 
     film_t = None
     if world > 1:
@@ -79,7 +79,7 @@ def main():
         rt.render(a.spp, tiles=tiles, first_sample=0)
         if world > 1:
             rt.copy_film_to(film_t.data_ptr())
-            dist.reduce(film_t, dst=0, op=dist.ReduceOp.SUM)
+            reduce_film(film_t, dist)
 
     def barrier_sync():
         if world > 1:

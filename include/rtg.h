@@ -146,6 +146,11 @@ int  rtg_get_stats(rtg_handle* h, rtg_stats* out);
  * Geometry.h:231-238). For any-hit, tmax is Scene::visible's maxT and the result is n int32
  * (1 = visible). Device-side arrays are allocated internally; inputs are host pointers. */
 int  rtg_trace_closest(rtg_handle* h, const float* rays, uint32_t n, float* hits);
+/* BSDF::sample / evaluate probe on the current device (Materials.h:118-318), scripted draws.
+ * cases: n*20 floats (kind, int_ior, ext_ior, albedo.rgb of a 1x1 texture, sNormal.xyz, wo.xyz,
+ * tu, tv, draw[4], pad[2]);
+ * out: n*11 floats (wi.xyz, reflectedColour.rgb, pdf, draws consumed, evaluate(wi).rgb). */
+int  rtg_probe_bsdf(const float* cases, uint32_t n, float* out);
 int  rtg_trace_visible(rtg_handle* h, const float* rays, uint32_t n, int32_t* visible);
 
 #ifdef __cplusplus

@@ -1,0 +1,116 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes access to oracle/_ref/libref.so (the reference's own
+headers compiled from /root/reference; only available in the build container)."""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_ref", "libref.so")
+LIB_RTM = os.path.join(HERE, "_ref", "libref_rtm.so")  # same code, shared transcendentals interposed
+
+
+def available():
+    return os.path.exists(LIB)
+
+
+_libs = {}
+
+
+def lib(flavour="libm"):
+    if flavour not in _libs:
+        L = C.CDLL(LIB if flavour == "libm" else LIB_RTM)
+        vp = C.c_void_p
+        L.ref_load.restype = vp
+        L.ref_load.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_char_p]
+        for name in ("ref_counts", "ref_export", "ref_texture_size", "ref_texture_texels", "ref_traverse",
+                     "ref_traverse_visible", "ref_visible", "ref_camera_rays", "ref_env_eval", "ref_tex_sample"):
+            getattr(L, name).restype = None
+        L.ref_bsdf_sample.restype = None
+        L.ref_save_hdr.restype = C.c_int
+        L.ref_load_texture.restype = C.c_int
+        _libs[flavour] = L
+    return _libs[flavour]
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class RefScene:
+    def __init__(self, scene_dir, width=0, height=0, skip_missing=False, envmap=None):
+        self.L = lib()
+        self.h = self.L.ref_load(os.fsencode(scene_dir), width, height, 1 if skip_missing else 0,
+                                 envmap.encode() if envmap else None)
+        c = np.zeros(8, np.int32)
+        self.L.ref_counts(C.c_void_p(self.h), _p(c))
+        self.ntri, self.nnode, self.nlight, self.nmat, self.ntex, self.env_tex, self.W, self.H = c.tolist()
+
+    def export(self):
+        n, m = self.ntri, self.nnode
+        d = {"positions": np.zeros((n, 3, 3), np.float32), "normals": np.zeros((n, 3, 3), np.float32),
+             "uvs": np.zeros((n, 3, 2), np.float32), "material": np.zeros(n, np.uint32),
+             "node_bounds": np.zeros((m, 6), np.float32), "node_links": np.zeros((m, 4), np.int32),
+             "lights": np.zeros(self.nlight, np.int32), "camera": np.zeros(37, np.float32),
+             "mat_info": np.zeros((self.nmat, 3), np.int32), "mat_f": np.zeros((self.nmat, 5), np.float32)}
+        self.L.ref_export(C.c_void_p(self.h), *[_p(d[k]) for k in ("positions", "normals", "uvs", "material", "node_bounds",
+                                                                 "node_links", "lights", "camera", "mat_info", "mat_f")])
+        return d
+
+    def texture(self, i):
+        wh = np.zeros(2, np.int32)
+        self.L.ref_texture_size(C.c_void_p(self.h), int(i), _p(wh))
+        out = np.zeros((wh[1], wh[0], 3), np.float32)
+        self.L.ref_texture_texels(C.c_void_p(self.h), int(i), _p(out))
+        return out
+
+    def traverse(self, rays):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        out = np.zeros((len(r), 4), np.float32)
+        self.L.ref_traverse(C.c_void_p(self.h), _p(r), len(r), _p(out))
+        return out
+
+    def traverse_visible(self, rays):
+        r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+        out = np.zeros(len(r), np.int32)
+        self.L.ref_traverse_visible(C.c_void_p(self.h), _p(r), len(r), _p(out))
+        return out
+
+    def camera_rays(self, pixels):
+        p = np.ascontiguousarray(pixels, np.uint32)
+        out = np.zeros((len(p), 6), np.float32)
+        self.L.ref_camera_rays(C.c_void_p(self.h), _p(p), len(p), _p(out))
+        return out
+
+    def env_eval(self, tex, dirs):
+        d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        out = np.zeros((len(d), 3), np.float32)
+        self.L.ref_env_eval(C.c_void_p(self.h), int(tex), _p(d), len(d), _p(out))
+        return out
+
+    def tex_sample(self, tex, uv):
+        u = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+        out = np.zeros((len(u), 3), np.float32)
+        self.L.ref_tex_sample(C.c_void_p(self.h), int(tex), _p(u), len(u), _p(out))
+        return out
+
+
+def bsdf_sample(kind, albedo, sd, draws, int_ior=1.33, ext_ior=1.0, flavour="libm"):
+    a = np.asarray(albedo, np.float32)
+    s = np.asarray(sd, np.float32)
+    d = np.asarray(draws, np.float32)
+    out = np.zeros(11, np.float32)
+    lib(flavour).ref_bsdf_sample(C.c_int(kind), _p(a), C.c_float(int_ior), C.c_float(ext_ior), _p(s), _p(d), C.c_int(len(d)), _p(out))
+    return out
+
+
+def save_hdr(path, film_sum, spp):
+    f = np.ascontiguousarray(film_sum, np.float32)
+    lib().ref_save_hdr(os.fsencode(path), f.shape[1], f.shape[0], _p(f), spp)
+
+
+def load_texture(path, cap=1 << 24):
+    out = np.zeros(cap, np.float32)
+    wh = np.zeros(2, np.int32)
+    n = lib().ref_load_texture(os.fsencode(path), _p(out), cap, _p(wh))
+    return out[: n * 3].reshape(wh[1], wh[0], 3)

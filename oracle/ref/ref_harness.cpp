@@ -1,0 +1,406 @@
+// ref_harness.cpp — TEST INFRASTRUCTURE ONLY (oracle/_ref). Builds RTBase's own code, compiled
+// straight from /root/reference/RTBase (no copies, no stand-in headers), and exposes it through a
+// C-ABI so tests/golden/make_golden.py can pin the product's host front-end and kernels:
+//
+//   compiled from the reference: Core.h (Matrix/Vec3/Frame), Geometry.h (Triangle::init,
+//   rayIntersect, AABB, BVHNode::build/traverse/traverseVisible), Scene.h (Camera, Scene::build,
+//   traverse, visible, calculateShadingData), Materials.h (all BSDFs), Lights.h, Imaging.h
+//   (Texture::load via the vendored stb_image, Film), GEMLoader.h (JSON + .gem).
+//
+// NOT compilable here: Renderer.h and SceneLoader.h include the Windows/D3D11-only
+// GamesEngineeringBase.h (windows.h, d3d11.h, XAudio2...). So loadScene's ~60-line glue
+// (SceneLoader.h:104-291) is restated below using the reference classes, and pathTrace /
+// computeDirect are not exercised here (the integrator is pinned by the survey's known answer).
+#include "GEMLoader.h"
+#include "Scene.h"
+
+#include <sys/stat.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace {
+
+struct ScriptSampler : Sampler {
+    const float* v;
+    int n, i = 0;
+    ScriptSampler(const float* vals, int count) : v(vals), n(count) {}
+    float next() override { return i < n ? v[i++] : 0.5f; }
+};
+
+bool exists(const std::string& p) {
+    struct stat st;
+    return ::stat(p.c_str(), &st) == 0;
+}
+
+Texture* load_tex(const std::string& fn, std::map<std::string, Texture*>& cache, std::vector<std::string>& names) {
+    auto it = cache.find(fn);
+    if (it != cache.end()) return it->second;
+    Texture* t = new Texture();
+    t->load(fn);
+    cache.insert({fn, t});
+    names.push_back(fn);
+    return t;
+}
+
+struct RefScene {
+    Scene* scene = nullptr;
+    std::vector<Texture*> textures;        // in first-use order
+    std::map<Texture*, int> tex_index;
+    std::vector<int> mat_kind, mat_two_sided, mat_tex;
+    std::vector<float> mat_ior;             // int, ext
+    int env_tex = -1;
+};
+
+// SceneLoader.h:104-235 restated on the reference classes.
+void load_instance(const std::string& dir, std::vector<Triangle>& tris, std::vector<BSDF*>& mats,
+                   GEMLoader::GEMInstance& inst, std::map<std::string, Texture*>& cache,
+                   std::vector<std::string>& names, bool skip_missing) {
+    if (skip_missing && (!exists(dir + "/" + inst.meshFilename) ||
+                         !exists(dir + "/" + inst.material.find("reflectance").getValue("")))) return;
+    GEMLoader::GEMModelLoader loader;
+    std::vector<GEMLoader::GEMMesh> meshes;
+    loader.load(dir + "/" + inst.meshFilename, meshes);
+    BSDF* material = NULL;
+    std::string bsdf = inst.material.find("bsdf").getValue("");
+    std::string fn = dir + "/" + inst.material.find("reflectance").getValue("");
+    if (bsdf == "diffuse") material = new DiffuseBSDF(load_tex(fn, cache, names));
+    if (bsdf == "orennayar") material = new OrenNayarBSDF(load_tex(fn, cache, names), inst.material.find("alpha").getValue(1.0f));
+    if (bsdf == "glass") material = new GlassBSDF(load_tex(fn, cache, names), inst.material.find("intIOR").getValue(1.33f), inst.material.find("extIOR").getValue(1.0f));
+    if (bsdf == "mirror") material = new MirrorBSDF(load_tex(fn, cache, names));
+    if (bsdf == "plastic") material = new PlasticBSDF(load_tex(fn, cache, names), inst.material.find("intIOR").getValue(1.33f), inst.material.find("extIOR").getValue(1.0f), inst.material.find("roughness").getValue(1.0f));
+    if (bsdf == "dielectric") {
+        float rough = inst.material.find("roughness").getValue(1.0f);
+        if (rough < 0.001f) material = new GlassBSDF(load_tex(fn, cache, names), inst.material.find("intIOR").getValue(1.33f), inst.material.find("extIOR").getValue(1.0f));
+        else material = new DielectricBSDF(load_tex(fn, cache, names), inst.material.find("intIOR").getValue(1.33f), inst.material.find("extIOR").getValue(1.0f), rough);
+    }
+    if (bsdf == "conductor") {
+        Colour eta, k;
+        inst.material.find("eta").getValuesAsVector3(eta.r, eta.g, eta.b);
+        inst.material.find("k").getValuesAsVector3(k.r, k.g, k.b);
+        material = new ConductorBSDF(load_tex(fn, cache, names), eta, k, inst.material.find("roughness").getValue(1.0f));
+    }
+    if (material == NULL) return;
+    mats.push_back(material);
+    if (inst.material.find("emission").getValue("") != "") {
+        Colour e;
+        inst.material.find("emission").getValuesAsVector3(e.r, e.g, e.b);
+        material->addLight(e);
+    }
+    int mi = (int)mats.size() - 1;
+    std::vector<Vertex> verts;
+    std::vector<unsigned int> idx;
+    Matrix transform;
+    memcpy(transform.m, inst.w.m, 16 * sizeof(float));
+    Matrix vt = transform.invert();
+    vt = vt.transpose();
+    for (size_t i = 0; i < meshes.size(); i++) {
+        for (size_t n = 0; n < meshes[i].verticesStatic.size(); n++) {
+            Vertex v;
+            const auto& g = meshes[i].verticesStatic[n];
+            v.p = Vec3(g.position.x, g.position.y, g.position.z);
+            v.normal = Vec3(g.normal.x, g.normal.y, g.normal.z);
+            v.p = transform.mulPoint(v.p);
+            v.normal = vt.mulVec(v.normal);
+            v.normal = v.normal.normalize();
+            v.u = g.u;
+            v.v = g.v;
+            verts.push_back(v);
+        }
+        int offset = (int)idx.size();
+        for (size_t n = 0; n < meshes[i].indices.size(); n++) idx.push_back(offset + meshes[i].indices[n]);
+    }
+    for (size_t i = 0; i + 2 < idx.size(); i += 3) {
+        Triangle t;
+        t.init(verts[idx[i]], verts[idx[i + 1]], verts[idx[i + 2]], mi);
+        if (t.area > 0) tris.push_back(t);
+    }
+}
+
+void flatten(BVHNode* n, std::vector<BVHNode*>& out) {
+    out.push_back(n);
+    if (n->l) flatten(n->l, out);
+    if (n->r) flatten(n->r, out);
+}
+
+}  // namespace
+
+extern "C" {
+
+void* ref_load(const char* dir_c, int W, int H, int skip_missing, const char* env_override) {
+    std::string dir(dir_c);
+    GEMLoader::GEMScene gs;
+    gs.load(dir + "/scene.json");
+    int width = gs.findProperty("width").getValue(1920);
+    int height = gs.findProperty("height").getValue(1080);
+    if (W > 0) width = W;
+    if (H > 0) height = H;
+    float fov = gs.findProperty("fov").getValue(45.0f);
+    Matrix P = Matrix::perspective(0.001f, 10000.0f, (float)width / (float)height, fov);
+    Vec3 from, to, up;
+    gs.findProperty("from").getValuesAsVector3(from.x, from.y, from.z);
+    gs.findProperty("to").getValuesAsVector3(to.x, to.y, to.z);
+    gs.findProperty("up").getValuesAsVector3(up.x, up.y, up.z);
+    Matrix V = Matrix::lookAt(from, to, up);
+    V = V.invert();
+    if (gs.findProperty("flipX").getValue(0) == 1) P.a[0][0] = -P.a[0][0];
+    RefScene* rs = new RefScene();
+    rs->scene = new Scene();
+    rs->scene->camera.init(P, width, height);
+    rs->scene->camera.updateView(V);
+    std::vector<Triangle> tris;
+    std::vector<BSDF*> mats;
+    std::map<std::string, Texture*> cache;
+    std::vector<std::string> names;
+    for (size_t i = 0; i < gs.instances.size(); i++)
+        load_instance(dir, tris, mats, gs.instances[i], cache, names, skip_missing != 0);
+    std::string env = env_override ? std::string(env_override) : gs.findProperty("envmap").getValue("");
+    Light* bg;
+    Texture* envt = nullptr;
+    if (env != "") {
+        envt = load_tex(dir + "/" + env, cache, names);
+        bg = new EnvironmentMap(envt);
+    } else {
+        bg = new BackgroundColour(Colour(0.0f, 0.0f, 0.0f));
+    }
+    rs->scene->init(tris, mats, bg);
+    rs->scene->build();
+    for (const auto& n : names) {
+        rs->tex_index[cache[n]] = (int)rs->textures.size();
+        rs->textures.push_back(cache[n]);
+    }
+    rs->env_tex = envt ? rs->tex_index[envt] : -1;
+    for (BSDF* b : rs->scene->materials) {
+        int kind = 1, tex = -1;
+        float ii = 0, ee = 0;
+        if (auto* d = dynamic_cast<DiffuseBSDF*>(b)) { kind = 0; tex = rs->tex_index[d->albedo]; }
+        else if (auto* m = dynamic_cast<MirrorBSDF*>(b)) { kind = 2; tex = rs->tex_index[m->albedo]; }
+        else if (auto* g = dynamic_cast<GlassBSDF*>(b)) { kind = 3; tex = rs->tex_index[g->albedo]; ii = g->intIOR; ee = g->extIOR; }
+        else if (auto* c = dynamic_cast<ConductorBSDF*>(b)) tex = rs->tex_index[c->albedo];
+        else if (auto* p = dynamic_cast<PlasticBSDF*>(b)) tex = rs->tex_index[p->albedo];
+        else if (auto* o = dynamic_cast<OrenNayarBSDF*>(b)) tex = rs->tex_index[o->albedo];
+        else if (auto* e = dynamic_cast<DielectricBSDF*>(b)) tex = rs->tex_index[e->albedo];
+        rs->mat_kind.push_back(kind);
+        rs->mat_two_sided.push_back(b->isTwoSided() ? 1 : 0);
+        rs->mat_tex.push_back(tex);
+        rs->mat_ior.push_back(ii);
+        rs->mat_ior.push_back(ee);
+    }
+    return rs;
+}
+
+// counts: ntri, nnodes, nlights, nmats, ntex, env_tex, width, height
+void ref_counts(void* h, int* out) {
+    RefScene* rs = (RefScene*)h;
+    std::vector<BVHNode*> nodes;
+    flatten(rs->scene->bvh, nodes);
+    out[0] = (int)rs->scene->triangles.size();
+    out[1] = (int)nodes.size();
+    out[2] = (int)rs->scene->lights.size();
+    out[3] = (int)rs->scene->materials.size();
+    out[4] = (int)rs->textures.size();
+    out[5] = rs->env_tex;
+    out[6] = (int)rs->scene->camera.width;
+    out[7] = (int)rs->scene->camera.height;
+}
+
+// Export the built Scene in the layout of include/rtg.h's rtg_scene_desc.
+void ref_export(void* h, float* pos, float* nrm, float* uv, uint32_t* mat, float* nb, int32_t* nl, int32_t* lights,
+                float* cam /* 16 invP + 16 camera + 3 origin + 2 size */, int32_t* mat_info /* kind, two_sided, tex */,
+                float* mat_f /* int_ior, ext_ior, emission rgb */) {
+    RefScene* rs = (RefScene*)h;
+    Scene* s = rs->scene;
+    for (size_t i = 0; i < s->triangles.size(); i++) {
+        const Triangle& t = s->triangles[i];
+        for (int k = 0; k < 3; k++) {
+            pos[i * 9 + k * 3 + 0] = t.vertices[k].p.x;
+            pos[i * 9 + k * 3 + 1] = t.vertices[k].p.y;
+            pos[i * 9 + k * 3 + 2] = t.vertices[k].p.z;
+            nrm[i * 9 + k * 3 + 0] = t.vertices[k].normal.x;
+            nrm[i * 9 + k * 3 + 1] = t.vertices[k].normal.y;
+            nrm[i * 9 + k * 3 + 2] = t.vertices[k].normal.z;
+            uv[i * 6 + k * 2 + 0] = t.vertices[k].u;
+            uv[i * 6 + k * 2 + 1] = t.vertices[k].v;
+        }
+        mat[i] = t.materialIndex;
+    }
+    std::vector<BVHNode*> nodes;
+    flatten(s->bvh, nodes);
+    std::map<BVHNode*, int> id;
+    for (size_t i = 0; i < nodes.size(); i++) id[nodes[i]] = (int)i;
+    for (size_t i = 0; i < nodes.size(); i++) {
+        BVHNode* n = nodes[i];
+        nb[i * 6 + 0] = n->bounds.min.x; nb[i * 6 + 1] = n->bounds.min.y; nb[i * 6 + 2] = n->bounds.min.z;
+        nb[i * 6 + 3] = n->bounds.max.x; nb[i * 6 + 4] = n->bounds.max.y; nb[i * 6 + 5] = n->bounds.max.z;
+        nl[i * 4 + 0] = n->l ? id[n->l] : -1;
+        nl[i * 4 + 1] = n->r ? id[n->r] : -1;
+        nl[i * 4 + 2] = n->l ? 0 : n->startIndex;
+        nl[i * 4 + 3] = n->l ? 0 : n->endIndex;
+    }
+    for (size_t i = 0; i < s->lights.size(); i++) {
+        AreaLight* a = dynamic_cast<AreaLight*>(s->lights[i]);
+        lights[i] = a ? (int32_t)(a->triangle - s->triangles.data()) : -1;
+    }
+    memcpy(cam, s->camera.inverseProjectionMatrix.m, 64);
+    memcpy(cam + 16, s->camera.camera.m, 64);
+    cam[32] = s->camera.origin.x; cam[33] = s->camera.origin.y; cam[34] = s->camera.origin.z;
+    cam[35] = s->camera.width; cam[36] = s->camera.height;
+    for (size_t i = 0; i < s->materials.size(); i++) {
+        mat_info[i * 3 + 0] = rs->mat_kind[i];
+        mat_info[i * 3 + 1] = rs->mat_two_sided[i];
+        mat_info[i * 3 + 2] = rs->mat_tex[i];
+        mat_f[i * 5 + 0] = rs->mat_ior[i * 2];
+        mat_f[i * 5 + 1] = rs->mat_ior[i * 2 + 1];
+        mat_f[i * 5 + 2] = s->materials[i]->emission.r;
+        mat_f[i * 5 + 3] = s->materials[i]->emission.g;
+        mat_f[i * 5 + 4] = s->materials[i]->emission.b;
+    }
+}
+
+void ref_texture_size(void* h, int i, int* wh) {
+    RefScene* rs = (RefScene*)h;
+    wh[0] = rs->textures[i]->width;
+    wh[1] = rs->textures[i]->height;
+}
+void ref_texture_texels(void* h, int i, float* out) {
+    RefScene* rs = (RefScene*)h;
+    Texture* t = rs->textures[i];
+    for (int k = 0; k < t->width * t->height; k++) {
+        out[k * 3] = t->texels[k].r; out[k * 3 + 1] = t->texels[k].g; out[k * 3 + 2] = t->texels[k].b;
+    }
+}
+
+// Scene::traverse over n rays (o.xyz, pad, dir.xyz, pad) -> (t, id bits, alpha, beta); id -1 on miss.
+void ref_traverse(void* h, const float* rays, int n, float* out) {
+    Scene* s = ((RefScene*)h)->scene;
+    for (int i = 0; i < n; i++) {
+        const float* r = rays + i * 8;
+        Ray ray(Vec3(r[0], r[1], r[2]), Vec3(r[4], r[5], r[6]));
+        IntersectionData is = s->traverse(ray);
+        int id = is.t < FLT_MAX ? (int)is.ID : -1;
+        out[i * 4] = is.t;
+        memcpy(&out[i * 4 + 1], &id, 4);
+        out[i * 4 + 2] = is.t < FLT_MAX ? is.alpha : 0.0f;
+        out[i * 4 + 3] = is.t < FLT_MAX ? is.beta : 0.0f;
+    }
+}
+
+// BVHNode::traverseVisible with an explicit (o, dir, maxT) ray: (o.xyz, maxT, dir.xyz, pad).
+void ref_traverse_visible(void* h, const float* rays, int n, int32_t* out) {
+    Scene* s = ((RefScene*)h)->scene;
+    for (int i = 0; i < n; i++) {
+        const float* r = rays + i * 8;
+        Ray ray(Vec3(r[0], r[1], r[2]), Vec3(r[4], r[5], r[6]));
+        out[i] = s->bvh->traverseVisible(ray, s->triangles, r[3]) ? 1 : 0;
+    }
+}
+
+// Scene::visible(p1, p2): pairs (p1.xyz, p2.xyz).
+void ref_visible(void* h, const float* pairs, int n, int32_t* out) {
+    Scene* s = ((RefScene*)h)->scene;
+    for (int i = 0; i < n; i++) {
+        const float* p = pairs + i * 6;
+        out[i] = s->visible(Vec3(p[0], p[1], p[2]), Vec3(p[3], p[4], p[5])) ? 1 : 0;
+    }
+}
+
+// Camera::generateRay at pixel centres: out (o.xyz, dir.xyz).
+void ref_camera_rays(void* h, const uint32_t* pixels, int n, float* out) {
+    Scene* s = ((RefScene*)h)->scene;
+    uint32_t W = (uint32_t)s->camera.width;
+    for (int i = 0; i < n; i++) {
+        float px = (pixels[i] % W) + 0.5f, py = (pixels[i] / W) + 0.5f;
+        Ray r = s->camera.generateRay(px, py);
+        out[i * 6] = r.o.x; out[i * 6 + 1] = r.o.y; out[i * 6 + 2] = r.o.z;
+        out[i * 6 + 3] = r.dir.x; out[i * 6 + 4] = r.dir.y; out[i * 6 + 5] = r.dir.z;
+    }
+}
+
+// BSDF::sample on a standalone material with a scripted sampler.
+// kind: 0 diffuse, 1 conductor stub, 2 mirror, 3 glass(int_ior, ext_ior), 4 plastic, 5 orennayar, 6 dielectric
+// albedo: 1x1 texture colour. sd: sNormal.xyz, wo.xyz, tu, tv. Returns wi.xyz, refl.rgb, pdf, draws used.
+void ref_bsdf_sample(int kind, const float* albedo, float int_ior, float ext_ior, const float* sd,
+                     const float* draws, int ndraws, float* out) {
+    Texture tex;
+    tex.alpha = NULL;
+    tex.width = 1;
+    tex.height = 1;
+    tex.channels = 3;
+    tex.texels = new Colour[1];
+    tex.texels[0] = Colour(albedo[0], albedo[1], albedo[2]);
+    BSDF* b = nullptr;
+    switch (kind) {
+    case 0: b = new DiffuseBSDF(&tex); break;
+    case 1: b = new ConductorBSDF(&tex, Colour(1, 1, 1), Colour(1, 1, 1), 0.5f); break;
+    case 2: b = new MirrorBSDF(&tex); break;
+    case 3: b = new GlassBSDF(&tex, int_ior, ext_ior); break;
+    case 4: b = new PlasticBSDF(&tex, int_ior, ext_ior, 0.5f); break;
+    case 5: b = new OrenNayarBSDF(&tex, 0.5f); break;
+    default: b = new DielectricBSDF(&tex, int_ior, ext_ior, 0.5f); break;
+    }
+    ShadingData s(Vec3(0, 0, 0), Vec3(sd[0], sd[1], sd[2]));
+    s.wo = Vec3(sd[3], sd[4], sd[5]);
+    s.tu = sd[6];
+    s.tv = sd[7];
+    s.bsdf = b;
+    s.frame.fromVector(s.sNormal);
+    ScriptSampler smp(draws, ndraws);
+    Colour refl;
+    float pdf = 0;
+    Vec3 wi = b->sample(s, smp, refl, pdf);
+    Colour ev = b->evaluate(s, wi);
+    out[0] = wi.x; out[1] = wi.y; out[2] = wi.z;
+    out[3] = refl.r; out[4] = refl.g; out[5] = refl.b;
+    out[6] = pdf;
+    out[7] = (float)smp.i;
+    out[8] = ev.r; out[9] = ev.g; out[10] = ev.b;
+    delete b;
+}
+
+// EnvironmentMap::evaluate and ::sample of texture i of a loaded scene.
+void ref_env_eval(void* h, int tex, const float* dirs, int n, float* out) {
+    RefScene* rs = (RefScene*)h;
+    EnvironmentMap env(rs->textures[tex]);
+    for (int i = 0; i < n; i++) {
+        Colour c = env.evaluate(Vec3(dirs[i * 3], dirs[i * 3 + 1], dirs[i * 3 + 2]));
+        out[i * 3] = c.r; out[i * 3 + 1] = c.g; out[i * 3 + 2] = c.b;
+    }
+}
+
+// Texture::sample of texture i.
+void ref_tex_sample(void* h, int tex, const float* uv, int n, float* out) {
+    RefScene* rs = (RefScene*)h;
+    for (int i = 0; i < n; i++) {
+        Colour c = rs->textures[tex]->sample(uv[i * 2], uv[i * 2 + 1]);
+        out[i * 3] = c.r; out[i * 3 + 1] = c.g; out[i * 3 + 2] = c.b;
+    }
+}
+
+// Film::save through the vendored stb_image_write (RGBE bytes).
+int ref_save_hdr(const char* path, int w, int h, const float* sum, int spp) {
+    Film f;
+    f.init(w, h, new BoxFilter());
+    memcpy(f.film, sum, (size_t)w * h * 12);
+    f.SPP = spp;
+    f.save(path);
+    return 0;
+}
+
+// stbi_loadf / stbi_load as Texture::load sees them.
+int ref_load_texture(const char* path, float* out, int cap, int* wh) {
+    Texture t;
+    t.width = 0;
+    t.height = 0;
+    t.load(path);
+    wh[0] = t.width;
+    wh[1] = t.height;
+    int n = t.width * t.height;
+    for (int k = 0; k < n && k * 3 + 2 < cap; k++) {
+        out[k * 3] = t.texels[k].r; out[k * 3 + 1] = t.texels[k].g; out[k * 3 + 2] = t.texels[k].b;
+    }
+    return n;
+}
+
+}  // extern "C"

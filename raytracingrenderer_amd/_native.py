@@ -77,6 +77,7 @@ RTG_EXPORTS = [
     ("rtg_get_stats", C.c_int, [C.c_void_p, C.POINTER(rtg_stats)]),
     ("rtg_trace_closest", C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
     ("rtg_trace_visible", C.c_int, [C.c_void_p, f32p, C.c_uint32, i32p]),
+    ("rtg_probe_bsdf", C.c_int, [f32p, C.c_uint32, f32p]),
 ]
 
 RTH_EXPORTS = [

@@ -103,7 +103,24 @@ def build_ref(force=False):
     return os.path.join(ORACLE, "_ref", "libref.so")
 
 
+def stage_assets():
+    """Copy reference scene data (not code) used by tests/bench into assets/ (git-ignored, travels
+    to the GPU box): coffee (config C5) and GI.hdr. Only when /root/reference is present."""
+    src = "/root/reference/RTBase"
+    dst = os.path.join(ROOT, "assets")
+    if not os.path.isdir(src):
+        return
+    os.makedirs(dst, exist_ok=True)
+    for name in ("coffee",):
+        if os.path.isdir(os.path.join(src, name)) and not os.path.isdir(os.path.join(dst, name)):
+            shutil.copytree(os.path.join(src, name), os.path.join(dst, name))
+    for f in ("GI.hdr",):
+        if os.path.exists(os.path.join(src, f)) and not os.path.exists(os.path.join(dst, f)):
+            shutil.copy(os.path.join(src, f), os.path.join(dst, f))
+
+
 def build_all(force=False, device=True):
+    stage_assets()
     build_host(force)
     if device:
         build_device(force)

@@ -128,12 +128,10 @@ struct SceneView {
 
 // ------------------------------------------------------------------ Texture::sample
 RTG_D v3 texel(const float* t, int i) { return mk(t[i * 3 + 0], t[i * 3 + 1], t[i * 3 + 2]); }
-RTG_D v3 tex_sample(const SceneView& s, int tex, float tu, float tv) {
-    DevTex ti = s.texinfo[tex];
-    const float* T = s.texels + (size_t)ti.off * 3;
+RTG_D v3 bilinear(const float* T, int w, int h, float tu, float tv) {
     float au = fabsf(tu), av = fabsf(tv);
-    float u = smax(0.0f, au) * (float)ti.w;
-    float v = smax(0.0f, av) * (float)ti.h;
+    float u = smax(0.0f, au) * (float)w;
+    float v = smax(0.0f, av) * (float)h;
     int x = (int)floorf(u);
     int y = (int)floorf(v);
     float fu = u - (float)x;
@@ -142,12 +140,16 @@ RTG_D v3 tex_sample(const SceneView& s, int tex, float tu, float tv) {
     float w1 = fu * (1.0f - fv);
     float w2 = (1.0f - fu) * fv;
     float w3 = fu * fv;
-    x = x % ti.w;
-    y = y % ti.h;
-    int x1 = (x + 1) % ti.w, y1 = (y + 1) % ti.h;
-    v3 s0 = texel(T, y * ti.w + x), s1 = texel(T, y * ti.w + x1);
-    v3 s2 = texel(T, y1 * ti.w + x), s3 = texel(T, y1 * ti.w + x1);
+    x = x % w;
+    y = y % h;
+    int x1 = (x + 1) % w, y1 = (y + 1) % h;
+    v3 s0 = texel(T, y * w + x), s1 = texel(T, y * w + x1);
+    v3 s2 = texel(T, y1 * w + x), s3 = texel(T, y1 * w + x1);
     return add(add(add(muls(s0, w0), muls(s1, w1)), muls(s2, w2)), muls(s3, w3));
+}
+RTG_D v3 tex_sample(const SceneView& s, int tex, float tu, float tv) {
+    DevTex ti = s.texinfo[tex];
+    return bilinear(s.texels + (size_t)ti.off * 3, ti.w, ti.h, tu, tv);
 }
 
 // ------------------------------------------------------------------ sampling (Sampling.h)
@@ -215,6 +217,62 @@ RTG_D uint64_t pcg_seed(uint64_t seed, uint64_t inc) {
 }
 RTG_D float pcg_next(uint64_t& s, uint64_t inc) {
     return (float)(pcg_step(s, inc) >> 8) * (1.0f / 16777216.0f);
+}
+
+// Sampler adaptors: the path's PCG stream, or a scripted list (probe / unit tests).
+struct PcgSampler {
+    uint64_t s;
+    uint64_t inc;
+    RTG_D float next() { return pcg_next(s, inc); }
+};
+struct ScriptSampler {
+    const float* v;
+    int n, i;
+    RTG_D float next() { return i < n ? v[i++] : 0.5f; }
+};
+
+// BSDF::sample for the three effective behaviours (Materials.h:127-134, 167-177, 218-226, 265-294,
+// 335-343, 380-388, 433-441). alb = albedo->sample(tu, tv). Returns wi (world); writes
+// reflectedColour and pdf. Draw order: Lambert family cosineSampleHemisphere(next(), next()) with
+// g++'s right-to-left argument evaluation (first draw -> r2); glass draws only when R != 1.
+template <class S>
+RTG_D v3 bsdf_sample(int kind, float int_ior, float ext_ior, v3 alb, const frame& fr, v3 wo, S& smp,
+                     v3& refl, float& pdf) {
+    if (kind == 0 || kind == 1) {  // RTG_MAT_DIFFUSE / RTG_MAT_LAMBERT
+        const float q2 = smp.next();
+        const float q1 = smp.next();
+        const v3 wl = cosine_sample_hemisphere(q1, q2);
+        if (kind == 0) pdf = (wl.z >= 0.0f) ? (float)((double)wl.z / RTM_PI) : 0.0f;  // cosineHemispherePDF
+        else pdf = (float)((double)wl.z / RTM_PI);                                      // stubs: wi.z / M_PI
+        refl = divs(alb, RTG_PI_F);
+        return to_world(fr, wl);
+    }
+    const v3 wol = to_local(fr, wo);
+    if (kind == 2) {  // RTG_MAT_MIRROR
+        pdf = 1.0f;
+        refl = alb;
+        return to_world(fr, mk(-wol.x, -wol.y, wol.z));
+    }
+    // RTG_MAT_GLASS
+    const float cos_i = fabsf(wol.z);
+    const bool enter = wol.z > 0.0f;
+    const float eta_i = enter ? ext_ior : int_ior;
+    const float eta_t = enter ? int_ior : ext_ior;
+    v3 wt = mk(0.0f, 0.0f, 0.0f);
+    const float R = fresnel_dielectric(cos_i, eta_i, eta_t, wt, wol);
+    if (!enter) wt.z = -wt.z;
+    const bool refl_dir = (R == 1.0f) || (smp.next() < R);
+    v3 wi;
+    if (refl_dir) {
+        wi = mk(-wol.x, -wol.y, wol.z);
+        pdf = R;
+        refl = muls(alb, R);
+    } else {
+        wi = wt;
+        pdf = 1.0f - R;
+        refl = muls(alb, 1.0f - R);
+    }
+    return to_world(fr, wi);
 }
 
 // ------------------------------------------------------------------ intersection

@@ -343,45 +343,12 @@ __global__ __launch_bounds__(RTG_TB) void k_shade(SceneView s, ChunkArgs a, Path
                         if (pcg_next(st, inc) < rrp) {
                             thr = divs(thr, rrp);
                             // ---- BSDF::sample
-                            v3 wi, ind;
+                            v3 ind;
                             float pdf;
-                            const v3 alb = tex_sample(s, M.tex, tu, tv);
-                            if (M.kind == RTG_MAT_DIFFUSE || M.kind == RTG_MAT_LAMBERT) {
-                                const float q2 = pcg_next(st, inc);  // cosineSampleHemisphere(next(), next())
-                                const float q1 = pcg_next(st, inc);
-                                const v3 wl = cosine_sample_hemisphere(q1, q2);
-                                if (M.kind == RTG_MAT_DIFFUSE)
-                                    pdf = (wl.z >= 0.0f) ? (float)((double)wl.z / RTM_PI) : 0.0f;
-                                else
-                                    pdf = (float)((double)wl.z / RTM_PI);
-                                ind = divs(alb, RTG_PI_F);
-                                wi = to_world(fr, wl);
-                            } else if (M.kind == RTG_MAT_MIRROR) {
-                                const v3 wol = to_local(fr, wo);
-                                pdf = 1.0f;
-                                ind = alb;
-                                wi = to_world(fr, mk(-wol.x, -wol.y, wol.z));
-                            } else {  // GLASS
-                                const v3 wol = to_local(fr, wo);
-                                const float cos_i = fabsf(wol.z);
-                                const bool enter = wol.z > 0.0f;
-                                const float eta_i = enter ? M.ext_ior : M.int_ior;
-                                const float eta_t = enter ? M.int_ior : M.ext_ior;
-                                v3 wt = mk(0.0f, 0.0f, 0.0f);
-                                const float R = fresnel_dielectric(cos_i, eta_i, eta_t, wt, wol);
-                                if (!enter) wt.z = -wt.z;
-                                const bool refl = (R == 1.0f) || (pcg_next(st, inc) < R);
-                                if (refl) {
-                                    wi = mk(-wol.x, -wol.y, wol.z);
-                                    pdf = R;
-                                    ind = muls(alb, R);
-                                } else {
-                                    wi = wt;
-                                    pdf = 1.0f - R;
-                                    ind = muls(alb, 1.0f - R);
-                                }
-                                wi = to_world(fr, wi);
-                            }
+                            PcgSampler smp{st, inc};
+                            const v3 wi = bsdf_sample(M.kind, M.int_ior, M.ext_ior, tex_sample(s, M.tex, tu, tv), fr, wo,
+                                                      smp, ind, pdf);
+                            st = smp.s;
                             if (spec) thr = divs(mul(thr, ind), pdf);
                             else thr = divs(muls(mul(thr, ind), fabsf(dot(wi, sn))), pdf);
                             const v3 no = add(x, muls(wi, RTG_EPS));
@@ -434,6 +401,30 @@ __global__ __launch_bounds__(RTG_TB) void k_accumulate(ChunkArgs a, PathBufs p, 
     film[(size_t)pixel * 3 + 0] = fr;
     film[(size_t)pixel * 3 + 1] = fg;
     film[(size_t)pixel * 3 + 2] = fb;
+}
+
+// BSDF probe: the exact device BSDF code on scripted inputs (unit parity vs RTBase's BSDF classes).
+// in: 20 floats per case = kind, int_ior, ext_ior, albedo.rgb (1x1 texture), sN.xyz, wo.xyz, tu, tv,
+//     draws[4], pad[2]; out: 11 floats = wi.xyz, refl.rgb, pdf, draws used, evaluate.rgb
+__global__ void k_probe_bsdf(const float* in, int n, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* c = in + (size_t)i * 20;
+    const int kind = (int)c[0];
+    const v3 alb = bilinear(c + 3, 1, 1, c[12], c[13]);  // albedo->sample(tu, tv)
+    const frame fr = frame_from(mk(c[6], c[7], c[8]));
+    const v3 wo = mk(c[9], c[10], c[11]);
+    ScriptSampler smp{c + 14, 4, 0};
+    v3 refl;
+    float pdf;
+    const v3 wi = bsdf_sample(kind, c[1], c[2], alb, fr, wo, smp, refl, pdf);
+    const v3 ev = kind <= 1 ? divs(alb, RTG_PI_F) : (kind == 2 ? alb : mk(0.0f, 0.0f, 0.0f));
+    float* o = out + (size_t)i * 11;
+    o[0] = wi.x; o[1] = wi.y; o[2] = wi.z;
+    o[3] = refl.x; o[4] = refl.y; o[5] = refl.z;
+    o[6] = pdf;
+    o[7] = (float)smp.i;
+    o[8] = ev.x; o[9] = ev.y; o[10] = ev.z;
 }
 
 // Per-chunk ray tally: extension + shadow queue lengths of every bounce into stats[2..3].
@@ -1057,6 +1048,22 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
     HIPOK(hipStreamSynchronize(h->stream));
     if (any) HIPOK(hipMemcpy(vis, d_out, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
     else HIPOK(hipMemcpy(hits, d_out, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return RTG_OK;
+}
+
+int rtg_probe_bsdf(const float* cases, uint32_t n, float* out) {
+    if (!cases || !out) return RTG_ERR_ARG;
+    if (n == 0) return RTG_OK;
+    float *d_in = nullptr, *d_out = nullptr;
+    HIPOK(hipMalloc((void**)&d_in, (size_t)n * 20 * sizeof(float)));
+    HIPOK(hipMalloc((void**)&d_out, (size_t)n * 11 * sizeof(float)));
+    HIPOK(hipMemcpy(d_in, cases, (size_t)n * 20 * sizeof(float), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_probe_bsdf, dim3((n + 255) / 256), dim3(256), 0, nullptr, d_in, (int)n, d_out);
+    HIPOK(hipGetLastError());
+    HIPOK(hipDeviceSynchronize());
+    HIPOK(hipMemcpy(out, d_out, (size_t)n * 11 * sizeof(float), hipMemcpyDeviceToHost));
     (void)hipFree(d_in);
     (void)hipFree(d_out);
     return RTG_OK;

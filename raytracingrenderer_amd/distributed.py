@@ -1,0 +1,34 @@
+"""Multi-GPU decomposition: 32x32 tiles interleaved over ranks + one film reduction.
+
+RTBase renders its 32x32 tiles (Renderer.h:18, 820-853) from a shared queue on CPU threads; here
+each rank (one process per GPU) owns tiles with tile_id % world == rank, renders all samples of
+them through its own librtg handle, and the float32 films are summed to rank 0 with a single
+torch.distributed reduce (RCCL over xGMI on MI355X, gloo in CPU tests). Tile supports are
+disjoint and every other rank contributes +0.0, so the reduced film is bit-identical to a
+single-GPU render whatever the reduction order.
+"""
+import numpy as np
+
+TILE = 32
+
+
+def tiles_for_rank(width, height, rank, world):
+    tx, ty = (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+    t = np.arange(tx * ty, dtype=np.uint32)
+    return t[t % world == rank]
+
+
+def reduce_film(film_tensor, dist, dst=0):
+    """Sum the per-rank films into rank `dst` (in place). film_tensor: torch tensor HxWx3 f32."""
+    dist.reduce(film_tensor, dst=dst, op=dist.ReduceOp.SUM)
+    return film_tensor
+
+
+def render_sharded(rt, n_samples, rank, world, dist=None, film_tensor=None, first_sample=0):
+    """Render this rank's tiles with RayTracer `rt`, then reduce to rank 0 (if world > 1)."""
+    tiles = tiles_for_rank(rt.width, rt.height, rank, world)
+    rt.render(n_samples, tiles=tiles, first_sample=first_sample)
+    if world > 1:
+        rt.copy_film_to(film_tensor.data_ptr())
+        reduce_film(film_tensor, dist)
+    return film_tensor

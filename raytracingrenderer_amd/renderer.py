@@ -41,11 +41,14 @@ class Scene:
         if h:
             N.rth().rth_free_scene(h)
 
-    # numpy views (no copy) of the flattened arrays
+    # numpy views (no copy) of the flattened arrays; each view keeps this Scene alive
     def _view(self, p, n, dtype):
         if n == 0:
             return np.zeros(0, dtype)
-        return np.ctypeslib.as_array(p, shape=(n,)).view(dtype)
+        ctype = p._type_
+        buf = (ctype * n).from_address(C.addressof(p.contents))
+        buf._owner = self
+        return np.frombuffer(buf, dtype=np.dtype(ctype)).view(dtype)
 
     @property
     def positions(self):

@@ -1,0 +1,125 @@
+"""Regenerate the golden fixtures in tests/golden/ (build container only).
+
+Sources of truth:
+  * oracle/_ref/libref.so — RTBase's own code compiled from /root/reference (loader classes,
+    Triangle/AABB/BVH, Scene::traverse/visible, Camera, BSDFs, EnvironmentMap, Texture, Film::save);
+  * SURVEY.md §8(c) known answer for C1 (pinned by the reference integrator built in the survey).
+The scene assets used are data files of the reference (RTBase/*/scene.json, .gem, .png, .hdr).
+
+Usage: python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+GOLD = os.path.join(ROOT, "tests", "golden")
+REF = "/root/reference/RTBase"
+
+from oracle import pyref  # noqa: E402
+from raytracingrenderer_amd import write_synthetic_scene  # noqa: E402
+
+SCENES = {
+    # name: (dir, width, height, skip_missing)
+    "cornell256": (os.path.join(GOLD, "scenes", "cornell-box"), 256, 256, False),
+    "synth20k": ("/tmp/rtg_golden_synth20k", 0, 0, False),
+    "coffee_f": (os.path.join(REF, "coffee"), 400, 500, True),
+    "bathroom_f": (os.path.join(REF, "bathroom"), 480, 270, True),
+}
+ARRAYS = ("positions", "normals", "uvs", "material", "node_bounds", "node_links", "lights", "camera")
+
+
+def digest(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def random_rays(rng, n, lo, hi, tmax=(0.05, 4.0)):
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    # a slice of axis-parallel and exactly-zero-component directions (inf invDir, NaN slab terms)
+    k = n // 16
+    d[:k] = np.eye(3, dtype=np.float32)[rng.integers(0, 3, k)] * rng.choice([-1, 1], (k, 1)).astype(np.float32)
+    d[k:2 * k, rng.integers(0, 3)] = 0.0
+    d[k:2 * k] /= np.linalg.norm(d[k:2 * k], axis=1, keepdims=True)
+    r = np.zeros((n, 8), np.float32)
+    r[:, :3] = o
+    r[:, 4:7] = d
+    r[:, 3] = rng.uniform(*tmax, n)
+    return r
+
+
+def main():
+    assert pyref.available(), "build oracle/_ref first (raytracingrenderer_amd.build.build_ref)"
+    write_synthetic_scene(SCENES["synth20k"][0], n_tris=20000, seed=3, width=128, height=96)
+    digests = {}
+    for name, (path, w, h, skip) in SCENES.items():
+        if not os.path.isdir(path):
+            continue
+        r = pyref.RefScene(path, w, h, skip)
+        d = r.export()
+        digests[name] = {k: digest(d[k]) for k in ARRAYS}
+        digests[name].update(n_tris=r.ntri, n_nodes=r.nnode, n_lights=r.nlight, width=r.W, height=r.H,
+                             mat_info=digest(d["mat_info"][:, :2]), mat_f=digest(d["mat_f"]))
+        if name in ("cornell256", "synth20k"):
+            rng = np.random.default_rng(12345)
+            lo, hi = (np.array([-1.5, -0.5, -1.5]), np.array([1.5, 2.5, 1.5])) if name == "cornell256" else (-1.3, 1.3)
+            rays = random_rays(rng, 4096, lo, hi)
+            pix = rng.integers(0, r.W * r.H, 4096).astype(np.uint32)
+            np.savez_compressed(os.path.join(GOLD, "%s_rays.npz" % name), rays=rays, hits=r.traverse(rays),
+                                visible=r.traverse_visible(rays), pixels=pix, camera_rays=r.camera_rays(pix),
+                                **({k: d[k] for k in ARRAYS} if name == "cornell256" else {}))
+    json.dump(digests, open(os.path.join(GOLD, "scene_digests.json"), "w"), indent=1, sort_keys=True)
+
+    # BSDF::sample / evaluate known answers (scripted sampler draws)
+    rng = np.random.default_rng(7)
+    kat = []
+    for kind in range(7):
+        for _ in range(24):
+            n = rng.normal(size=3); n /= np.linalg.norm(n)
+            wo = rng.normal(size=3); wo /= np.linalg.norm(wo)
+            sd = np.concatenate([n, wo, rng.uniform(0, 3, 2)]).astype(np.float32)
+            draws = rng.random(4).astype(np.float32)
+            if rng.random() < 0.1:
+                draws[:2] = 0.0  # r1 = 0 -> theta = acos(0) -> cos(theta) slightly negative (pdf quirk)
+            alb = rng.uniform(0.05, 1, 3).astype(np.float32)
+            ii, ee = (1.5, 1.0) if rng.random() < 0.5 else (1.33, 1.0)
+            out = pyref.bsdf_sample(kind, alb, sd, draws, ii, ee, "libm")
+            out_rtm = pyref.bsdf_sample(kind, alb, sd, draws, ii, ee, "rtm")
+            kat.append({"kind": kind, "albedo": alb.tolist(), "sd": sd.tolist(), "draws": draws.tolist(),
+                        "int_ior": ii, "ext_ior": ee, "out": out.tolist(),
+                        "out_bits_libm": out.view(np.uint32).tolist(),
+                        "out_bits_rtm": out_rtm.view(np.uint32).tolist()})
+    json.dump(kat, open(os.path.join(GOLD, "bsdf_kat.json"), "w"))
+
+    # Texture decode + sample, EnvironmentMap::evaluate, Film::save bytes
+    env_dir = os.path.join(GOLD, "scenes", "cornell-mat")
+    rs = pyref.RefScene(env_dir, 64, 48, False)
+    tex_kat = {}
+    dirs = rng.normal(size=(2048, 3)).astype(np.float32)
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    dirs[:8] = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1], [0, 1.0000001, 0], [-1, -0.0, 0]], np.float32)
+    uv = rng.uniform(-3, 3, (2048, 2)).astype(np.float32)
+    np.savez_compressed(os.path.join(GOLD, "env_tex_kat.npz"), dirs=dirs, env=rs.env_eval(rs.env_tex, dirs), uv=uv,
+                        tex=rs.tex_sample(rs.env_tex, uv))
+    for fn in ("bathroom/floor_tiles.png", "bathroom/rug_mask.png", "GI.hdr", "materialball/envmap.hdr"):
+        p = os.path.join(REF, fn)
+        if os.path.exists(p):
+            t = pyref.load_texture(p)
+            tex_kat[fn] = {"shape": list(t.shape), "sha256": digest(t)}
+    json.dump(tex_kat, open(os.path.join(GOLD, "texture_decode_kat.json"), "w"), indent=1)
+    film = np.random.default_rng(3).gamma(0.5, 2.0, (24, 40, 3)).astype(np.float32)
+    film[0, :5] = 0.0
+    film[1, :] = film[1, 0]  # long runs for the RLE encoder
+    pyref.save_hdr("/tmp/rtg_golden_film.hdr", film, 3)
+    np.savez_compressed(os.path.join(GOLD, "rgbe_kat.npz"), film=film, spp=3,
+                        hdr=np.frombuffer(open("/tmp/rtg_golden_film.hdr", "rb").read(), np.uint8))
+    print("golden fixtures written to", GOLD)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,44 @@
+"""The C-ABI boundary: every function declared in include/*.h is exported by the built libraries,
+the ABI version matches, and without a GPU the render path fails loudly (no CPU fallback)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT, has_gpu
+from raytracingrenderer_amd import _native as N
+
+
+def declared(header):
+    text = open(os.path.join(ROOT, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return set(re.findall(r"\b((?:rtg|rth)_[a-z_]+)\s*\(", text))
+
+
+@pytest.mark.parametrize("header,lib", [("rtg.h", "librtg.so"), ("rth.h", "librth.so")])
+def test_exports_cover_header(header, lib):
+    path = os.path.join(N.LIB_DIR, lib)
+    if lib == "librtg.so" and not os.path.exists(path):
+        pytest.skip("hipcc not available")
+    so = C.CDLL(path)
+    names = declared(header)
+    assert names, header
+    missing = [n for n in sorted(names) if not hasattr(so, n)]
+    assert not missing, missing
+    bound = {e[0] for e in (N.RTG_EXPORTS if lib == "librtg.so" else N.RTH_EXPORTS)}
+    assert names <= bound | {"rtg_abi_version"}, names - bound
+
+
+def test_abi_version():
+    assert N.rtg().rtg_abi_version() == 1
+
+
+def test_no_gpu_fails_loudly():
+    if has_gpu():
+        pytest.skip("a GPU is present")
+    from raytracingrenderer_amd import NativeError, RayTracer, loadScene
+    from conftest import SCENES
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=32, height=32)
+    with pytest.raises(NativeError):
+        RayTracer(s)
