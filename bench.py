@@ -95,7 +95,7 @@ def main():
     # timed region: per-launch HIP events on the render stream give the closest-hit kernel time
     rt.set_options(flags=N.RTG_OPT_CULL | N.RTG_OPT_TIMING)
     ext_rays = shadow_rays = paths = 0
-    extend_ms = 0.0
+    extend_ms = shadow_ms = shade_ms = 0.0
     extend_launches = 0
     barrier_sync()
     t_start = time.perf_counter()
@@ -106,6 +106,8 @@ def main():
         shadow_rays += st["shadow_rays"]
         paths += st["paths"]
         extend_ms += st["extend_ms"]
+        shadow_ms += st["shadow_ms"]
+        shade_ms += st["shade_ms"]
         extend_launches += st["extend_launches"]
     barrier_sync()
     elapsed = time.perf_counter() - t_start
@@ -180,6 +182,9 @@ def main():
                          "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
                          "tri_tests_per_ray": round(tris_per_ray, 2),
                          "avg_launch_ms": round(extend_ms / max(extend_launches, 1), 4)},
+            "kernel_ms_per_step": {"closest_hit": round(extend_ms / a.steps / world, 2),
+                                   "any_hit": round(shadow_ms / a.steps / world, 2),
+                                   "generate_shade_accumulate": round(shade_ms / a.steps / world, 2)},
             "cpu_baseline": cpu,
             "setup_s": round(setup_s, 2),
         }
