@@ -120,6 +120,7 @@ def main():
     cs = rt.stats()
     rt.set_options(flags=N.RTG_OPT_CULL)
 
+    local_kernel_ms = (extend_ms, shadow_ms, shade_ms)
     totals = np.array([ext_rays, shadow_rays, paths, extend_ms, extend_launches,
                        cs["node_visits"], cs["tri_tests"], cs["extension_rays"]], dtype=np.float64)
     t_max = elapsed
@@ -182,9 +183,9 @@ def main():
                          "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
                          "tri_tests_per_ray": round(tris_per_ray, 2),
                          "avg_launch_ms": round(extend_ms / max(extend_launches, 1), 4)},
-            "kernel_ms_per_step": {"closest_hit": round(extend_ms / a.steps / world, 2),
-                                   "any_hit": round(shadow_ms / a.steps / world, 2),
-                                   "generate_shade_accumulate": round(shade_ms / a.steps / world, 2)},
+            "kernel_ms_per_step_rank0": {"closest_hit": round(local_kernel_ms[0] / a.steps, 2),
+                                         "any_hit": round(local_kernel_ms[1] / a.steps, 2),
+                                         "generate_shade_accumulate": round(local_kernel_ms[2] / a.steps, 2)},
             "cpu_baseline": cpu,
             "setup_s": round(setup_s, 2),
         }

@@ -122,7 +122,7 @@ def rtg():
     """The HIP library. Raises if missing: there is no CPU fallback for the render path."""
     global _rtg
     if _rtg is None:
-        path = os.path.join(LIB_DIR, "librtg.so")
+        path = os.environ.get("RTG_LIB") or os.path.join(LIB_DIR, "librtg.so")  # RTG_LIB: A/B builds
         if not os.path.exists(path):
             raise ImportError("librtg.so not built (run raytracingrenderer_amd.build)")
         _rtg = _bind(C.CDLL(path, mode=C.RTLD_GLOBAL), RTG_EXPORTS)

@@ -15,6 +15,12 @@
 #include <stdint.h>
 
 #include "../../../include/rtg_math.h"
+#ifdef RTG_TIMING_ONLY_FAST_MATH  // A/B experiment only: NOT bit-faithful, never shipped
+#define rtm_sinf(x) __sinf(x)
+#define rtm_cosf(x) __cosf(x)
+#define rtm_acosf(x) acosf(x)
+#define rtm_atan2f(y, x) atan2f(y, x)
+#endif
 
 #define RTG_D __device__ __forceinline__
 #define RTG_FLT_MAX 3.40282347e+38f

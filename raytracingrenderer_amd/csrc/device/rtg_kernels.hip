@@ -37,19 +37,24 @@ using namespace rtgd;
 #define RTG_TB 256          // threads per block (4 waves)
 #define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (24 KB per block)
 #define RTG_CULL_REL 1.52587890625e-05f  // 2^-16 relative inflation for distance culling
+#ifndef RTG_SHADE_WAVES
+#define RTG_SHADE_WAVES 4                // min waves per SIMD for k_shade (register budget)
+#endif
 
-struct __align__(16) ExtRay { float4 o; float4 d; };            // o.w = path id bits
-struct __align__(16) ShadowRay { float4 o; float4 d; float4 c; }; // o.w = maxT, d.w = path id, c = NEE value
 struct __align__(16) Counters { unsigned n_ext, n_shadow, f_ext, f_shadow, f_shade, pad0, pad1, pad2; };
 
+// Queues hold path ids only; ray payloads live in per-path arrays (written in place by k_shade),
+// so compaction moves 4 bytes per ray and needs one atomic per 256 paths.
 struct TraceIO {
-    const ExtRay* ext;         // closest-hit input
-    const ShadowRay* sh;       // any-hit input
+    const unsigned* queue;     // path ids to trace
+    const float4* ray_o;       // [pid] origin.xyz, w = maxT (any-hit)
+    const float4* ray_d;       // [pid] direction.xyz
+    const float4* ray_c;       // [pid] any-hit: NEE value copied to contrib[pid] when visible
     const unsigned* count;     // number of rays (device)
     unsigned* fetch;           // work counter (device, zeroed)
-    float4* hits;              // closest-hit output
-    float4* contrib;           // any-hit: write ShadowRay.c to contrib[pid] when visible
-    int* visible;              // any-hit query output (instead of contrib)
+    float4* hits;              // closest-hit output [pid]
+    float4* contrib;           // any-hit: this bounce's contribution plane [pid]
+    int* visible;              // any-hit query output [pid] (instead of contrib)
     int* ovf;                  // global stack overflow [level][thread]
     unsigned long long* stats; // [0,1] closest / [4,5] any-hit: box tests, triangle tests (COUNT)
     int cull;
@@ -68,9 +73,14 @@ struct PathBufs {
     unsigned long long* rng;   // [P] PCG state
     int* meta;                 // [P] nterms | canHitLight << 8
     float4* contrib;           // [maxb][P] per-vertex radiance terms
-    ExtRay* q[2];              // extension queues (ping-pong)
-    float4* hits;              // [P]
-    ShadowRay* shq;            // [P]
+    float4* ray_o;             // [P] current extension ray origin
+    float4* ray_d;             // [P] current extension ray direction
+    float4* hits;              // [P] its closest hit (t, id, alpha, beta)
+    float4* sh_o;              // [P] NEE shadow ray origin + maxT
+    float4* sh_d;              // [P] NEE shadow ray direction
+    float4* sh_c;              // [P] NEE value thr * Ld if visible
+    unsigned* q[2];            // extension queues of path ids (ping-pong)
+    unsigned* shq;             // shadow queue of path ids
     Counters* ctr;             // [maxb + 1]
 };
 
@@ -78,6 +88,7 @@ static __device__ __forceinline__ int lane_id() { return __lane_id(); }
 static __device__ __forceinline__ unsigned prefix_lt(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
+
 
 // ------------------------------------------------------------------ traversal
 // Persistent lanes with per-lane ray replacement: a wave takes 64 ray indices at a time from the
@@ -101,15 +112,14 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
     float tbest = 0.0f, omag = 0.0f, dmag = 0.0f, delta = 0.0f, bu = 0.0f, bv = 0.0f;
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0;
     bool occluded = false;
-    float4 shc = make_float4(0, 0, 0, 0);
     for (;;) {
         // ---- retire finished rays
         if (have && cur == RTG_EXIT) {
             if (ANY) {
-                if (io.visible) io.visible[ri] = occluded ? 0 : 1;
-                else if (!occluded) io.contrib[pid] = shc;
+                if (io.visible) io.visible[pid] = occluded ? 0 : 1;
+                else if (!occluded) io.contrib[pid] = io.ray_c[pid];
             } else {
-                io.hits[ri] = make_float4(tbest, __int_as_float(bid), bu, bv);
+                io.hits[pid] = make_float4(tbest, __int_as_float(bid), bu, bv);
             }
             have = false;
         }
@@ -133,19 +143,11 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
                 if (!have && pos < take) {
                     ri = pool_base + pos;
                     have = true;
-                    if (ANY) {
-                        const ShadowRay r = io.sh[ri];
-                        o = mk(r.o.x, r.o.y, r.o.z);
-                        d = mk(r.d.x, r.d.y, r.d.z);
-                        tbest = r.o.w;
-                        pid = __float_as_int(r.d.w);
-                        shc = r.c;
-                    } else {
-                        const ExtRay r = io.ext[ri];
-                        o = mk(r.o.x, r.o.y, r.o.z);
-                        d = mk(r.d.x, r.d.y, r.d.z);
-                        tbest = RTG_FLT_MAX;
-                    }
+                    pid = (int)io.queue[ri];
+                    const float4 ro = io.ray_o[pid], rd = io.ray_d[pid];
+                    o = mk(ro.x, ro.y, ro.z);
+                    d = mk(rd.x, rd.y, rd.z);
+                    tbest = ANY ? ro.w : RTG_FLT_MAX;
                     inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // Ray::init
                     omag = s.cull_scale + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
                     dmag = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
@@ -260,35 +262,34 @@ __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
              (dir.x * c[4] + dir.y * c[5]) + dir.z * c[6],
              (dir.x * c[8] + dir.y * c[9]) + dir.z * c[10]);
     dir = normalize(dir);
-    ExtRay r;
-    r.o = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, __int_as_float((int)pid));
-    r.d = make_float4(dir.x, dir.y, dir.z, 0.0f);
-    p.q[0][pid] = r;
+    p.ray_o[pid] = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f);
+    p.ray_d[pid] = make_float4(dir.x, dir.y, dir.z, 0.0f);
+    p.q[0][pid] = pid;
     p.thr[pid] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
     p.rng[pid] = pcg_seed(a.seed, pcg_inc(pixel, a.s0 + sl));
     p.meta[pid] = 1 << 8;  // canHitLight = true
 }
 
 // ------------------------------------------------------------------ shade
-__global__ __launch_bounds__(RTG_TB) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
+__global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
+    __shared__ unsigned s_cnt[2][RTG_TB / 64];
+    __shared__ unsigned s_base[2];
     const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
     const unsigned n = p.ctr[b].n_ext;
-    const ExtRay* qin = p.q[b & 1];
-    ExtRay* qout = p.q[(b + 1) & 1];
+    const unsigned* qin = p.q[b & 1];
+    unsigned* qout = p.q[(b + 1) & 1];
     float4* contrib = p.contrib + (size_t)b * a.P;
-    const unsigned wave_global = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const unsigned waves = (gridDim.x * blockDim.x) >> 6;
-    for (unsigned base = wave_global * 64; base < n; base += waves * 64) {
-        const unsigned i = base + lane;
-        bool want_ext = false, want_sh = false;
-        ExtRay next_ray;
-        ShadowRay shr;
+    // block-uniform loop: all waves of a block take part in every compaction round
+    for (unsigned base = blockIdx.x * RTG_TB; base < n; base += gridDim.x * RTG_TB) {
+        const unsigned i = base + threadIdx.x;
         int pid = 0;
+        bool want_ext = false, want_sh = false;
         if (i < n) {
-            const ExtRay r = qin[i];
-            const float4 h = p.hits[i];
-            pid = __float_as_int(r.o.w);
-            const v3 o = mk(r.o.x, r.o.y, r.o.z), d = mk(r.d.x, r.d.y, r.d.z);
+            pid = (int)qin[i];
+            const float4 ro = p.ray_o[pid], rd = p.ray_d[pid];
+            const float4 h = p.hits[pid];
+            const v3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
             const float4 thr4 = p.thr[pid];
             v3 thr = mk(thr4.x, thr4.y, thr4.z);
             const int can_hit = (p.meta[pid] >> 8) & 1;
@@ -361,9 +362,9 @@ __global__ __launch_bounds__(RTG_TB) void k_shade(SceneView s, ChunkArgs a, Path
                             const v3 f = divs(tex_sample(s, M.tex, tu, tv), RTG_PI_F);  // BSDF::evaluate
                             ld = divs(muls(mul(f, emitted), g), pmf * pdf);
                             const v3 cvis = mul(thr, ld);
-                            shr.o = make_float4(so.x, so.y, so.z, maxt);
-                            shr.d = make_float4(sd.x, sd.y, sd.z, __int_as_float(pid));
-                            shr.c = make_float4(cvis.x, cvis.y, cvis.z, 0.0f);
+                            p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
+                            p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 0.0f);
+                            p.sh_c[pid] = make_float4(cvis.x, cvis.y, cvis.z, 0.0f);
                             want_sh = true;
                         }
                     }
@@ -383,8 +384,8 @@ __global__ __launch_bounds__(RTG_TB) void k_shade(SceneView s, ChunkArgs a, Path
                             if (spec) thr = divs(mul(thr, ind), pdf);
                             else thr = divs(muls(mul(thr, ind), fabsf(dot(wi, sn))), pdf);
                             const v3 no = add(x, muls(wi, RTG_EPS));
-                            next_ray.o = make_float4(no.x, no.y, no.z, __int_as_float(pid));
-                            next_ray.d = make_float4(wi.x, wi.y, wi.z, 0.0f);
+                            p.ray_o[pid] = make_float4(no.x, no.y, no.z, 0.0f);
+                            p.ray_d[pid] = make_float4(wi.x, wi.y, wi.z, 0.0f);
                             want_ext = true;
                             p.thr[pid] = make_float4(thr.x, thr.y, thr.z, 0.0f);
                             p.rng[pid] = st;
@@ -396,18 +397,32 @@ __global__ __launch_bounds__(RTG_TB) void k_shade(SceneView s, ChunkArgs a, Path
             contrib[pid] = make_float4(c.x, c.y, c.z, 0.0f);
             p.meta[pid] = nterms;
         }
-        // ---- wave-level compaction into the next queues (converged here)
+        // ---- block-level compaction of path ids into the next queues (one atomic per queue)
         const unsigned long long me = __ballot(want_ext);
         const unsigned long long ms = __ballot(want_sh);
-        unsigned be = 0, bs = 0;
         if (lane == 0) {
-            if (me) be = atomicAdd(&p.ctr[b + 1].n_ext, (unsigned)__popcll(me));
-            if (ms) bs = atomicAdd(&p.ctr[b].n_shadow, (unsigned)__popcll(ms));
+            s_cnt[0][wave] = (unsigned)__popcll(me);
+            s_cnt[1][wave] = (unsigned)__popcll(ms);
         }
-        be = __shfl(be, 0);
-        bs = __shfl(bs, 0);
-        if (want_ext) qout[be + prefix_lt(me)] = next_ray;
-        if (want_sh) p.shq[bs + prefix_lt(ms)] = shr;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned te = 0, ts = 0;
+            for (int w = 0; w < RTG_TB / 64; ++w) {
+                te += s_cnt[0][w];
+                ts += s_cnt[1][w];
+            }
+            s_base[0] = te ? atomicAdd(&p.ctr[b + 1].n_ext, te) : 0u;
+            s_base[1] = ts ? atomicAdd(&p.ctr[b].n_shadow, ts) : 0u;
+        }
+        __syncthreads();
+        unsigned oe = s_base[0], os = s_base[1];
+        for (int w = 0; w < wave; ++w) {
+            oe += s_cnt[0][w];
+            os += s_cnt[1][w];
+        }
+        if (want_ext) qout[oe + prefix_lt(me)] = (unsigned)pid;
+        if (want_sh) p.shq[os + prefix_lt(ms)] = (unsigned)pid;
+        __syncthreads();
     }
 }
 
@@ -530,6 +545,8 @@ struct rtg_handle {
 static void free_chunk(rtg_handle* h) {
     (void)hipFree(h->pb.thr); (void)hipFree(h->pb.rng); (void)hipFree(h->pb.meta); (void)hipFree(h->pb.contrib);
     (void)hipFree(h->pb.q[0]); (void)hipFree(h->pb.q[1]); (void)hipFree(h->pb.hits); (void)hipFree(h->pb.shq); (void)hipFree(h->pb.ctr);
+    (void)hipFree(h->pb.ray_o); (void)hipFree(h->pb.ray_d);
+    (void)hipFree(h->pb.sh_o); (void)hipFree(h->pb.sh_d); (void)hipFree(h->pb.sh_c);
     h->pb = PathBufs{};
     h->cap_P = 0;
     h->cap_maxb = 0;
@@ -543,10 +560,15 @@ static int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
     HIPOK(hipMalloc((void**)&p.rng, P * sizeof(unsigned long long)));
     HIPOK(hipMalloc((void**)&p.meta, P * sizeof(int)));
     HIPOK(hipMalloc((void**)&p.contrib, P * (size_t)maxb * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.q[0], P * sizeof(ExtRay)));
-    HIPOK(hipMalloc((void**)&p.q[1], P * sizeof(ExtRay)));
+    HIPOK(hipMalloc((void**)&p.q[0], P * sizeof(unsigned)));
+    HIPOK(hipMalloc((void**)&p.q[1], P * sizeof(unsigned)));
+    HIPOK(hipMalloc((void**)&p.shq, P * sizeof(unsigned)));
     HIPOK(hipMalloc((void**)&p.hits, P * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.shq, P * sizeof(ShadowRay)));
+    HIPOK(hipMalloc((void**)&p.ray_o, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.ray_d, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.sh_o, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.sh_d, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.sh_c, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.ctr, (size_t)(maxb + 1) * sizeof(Counters)));
     h->cap_P = P;
     h->cap_maxb = maxb;
@@ -906,7 +928,9 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
         LAUNCH_OK("k_generate");
         timed_end(h, st, k); kinds.push_back(2); ++k;
         for (int b = 0; b < maxb; ++b) {
-            io.ext = h->pb.q[b & 1];
+            io.queue = h->pb.q[b & 1];
+            io.ray_o = h->pb.ray_o;
+            io.ray_d = h->pb.ray_d;
             io.count = &h->pb.ctr[b].n_ext;
             io.fetch = &h->pb.ctr[b].f_ext;
             io.hits = h->pb.hits;
@@ -920,7 +944,10 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
             LAUNCH_OK("k_shade");
             timed_end(h, st, k); kinds.push_back(2); ++k;
             TraceIO sio = io;
-            sio.sh = h->pb.shq;
+            sio.queue = h->pb.shq;
+            sio.ray_o = h->pb.sh_o;
+            sio.ray_d = h->pb.sh_d;
+            sio.ray_c = h->pb.sh_c;
             sio.count = &h->pb.ctr[b].n_shadow;
             sio.fetch = &h->pb.ctr[b].f_shadow;
             sio.contrib = h->pb.contrib + (size_t)b * a.P;
@@ -1033,28 +1060,26 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
     if (!h || !rays || (!hits && !vis)) return RTG_ERR_ARG;
     if (n == 0) return RTG_OK;
     HIPOK(hipSetDevice(h->device));
-    void* d_in = nullptr;
+    // path-id indirection of the trace kernels: identity queue over n query rays
+    float4 *d_o = nullptr, *d_d = nullptr;
+    unsigned* d_q = nullptr;
     void* d_out = nullptr;
-    size_t in_bytes = (size_t)n * (any ? sizeof(ShadowRay) : sizeof(ExtRay));
-    HIPOK(hipMalloc(&d_in, in_bytes));
+    HIPOK(hipMalloc((void**)&d_o, (size_t)n * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&d_d, (size_t)n * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&d_q, (size_t)n * sizeof(unsigned)));
     HIPOK(hipMalloc(&d_out, (size_t)n * (any ? sizeof(int) : sizeof(float4))));
-    if (any) {
-        std::vector<ShadowRay> v(n);
+    {
+        std::vector<float4> vo(n), vd(n);
+        std::vector<unsigned> q(n);
         for (uint32_t i = 0; i < n; ++i) {
             const float* r = rays + (size_t)i * 8;
-            v[i].o = make_float4(r[0], r[1], r[2], r[3]);
-            v[i].d = make_float4(r[4], r[5], r[6], host_bits_f(0));
-            v[i].c = make_float4(0, 0, 0, 0);
+            vo[i] = make_float4(r[0], r[1], r[2], any ? r[3] : 0.0f);
+            vd[i] = make_float4(r[4], r[5], r[6], 0.0f);
+            q[i] = i;
         }
-        HIPOK(hipMemcpy(d_in, v.data(), in_bytes, hipMemcpyHostToDevice));
-    } else {
-        std::vector<ExtRay> v(n);
-        for (uint32_t i = 0; i < n; ++i) {
-            const float* r = rays + (size_t)i * 8;
-            v[i].o = make_float4(r[0], r[1], r[2], 0.0f);
-            v[i].d = make_float4(r[4], r[5], r[6], 0.0f);
-        }
-        HIPOK(hipMemcpy(d_in, v.data(), in_bytes, hipMemcpyHostToDevice));
+        HIPOK(hipMemcpy(d_o, vo.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice));
+        HIPOK(hipMemcpy(d_d, vd.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice));
+        HIPOK(hipMemcpy(d_q, q.data(), (size_t)n * sizeof(unsigned), hipMemcpyHostToDevice));
     }
     unsigned hc[4] = {n, 0, 0, 0};
     HIPOK(hipMemcpy(h->d_qctr, hc, sizeof(hc), hipMemcpyHostToDevice));
@@ -1066,12 +1091,13 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
     io.ovf = h->d_ovf;
     io.stats = h->d_stats;
     io.cull = h->cull;
+    io.queue = d_q;
+    io.ray_o = d_o;
+    io.ray_d = d_d;
     if (any) {
-        io.sh = (const ShadowRay*)d_in;
         io.visible = (int*)d_out;
         hipLaunchKernelGGL((k_trace<true, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, io);
     } else {
-        io.ext = (const ExtRay*)d_in;
         io.hits = (float4*)d_out;
         hipLaunchKernelGGL((k_trace<false, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, io);
     }
@@ -1079,7 +1105,9 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
     HIPOK(hipStreamSynchronize(h->stream));
     if (any) HIPOK(hipMemcpy(vis, d_out, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
     else HIPOK(hipMemcpy(hits, d_out, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));
-    (void)hipFree(d_in);
+    (void)hipFree(d_o);
+    (void)hipFree(d_d);
+    (void)hipFree(d_q);
     (void)hipFree(d_out);
     return RTG_OK;
 }

@@ -1,0 +1,8 @@
+#!/bin/bash
+# A/B: bench each lib variant in raytracingrenderer_amd/lib/ab (interleaved, 2 rounds)
+R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out; cd $R
+for round in 1 2; do
+for lib in raytracingrenderer_amd/lib/ab/*.so; do
+  RTG_LIB=$R/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps 3 $BENCH_ARGS > gpurun_out/ab.log 2>&1 || { tail -5 gpurun_out/ab.log; exit 1; }
+  echo "$(basename $lib) $(tail -1 gpurun_out/ab.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['kernel_ms_per_step_rank0'])")"
+done; done
