@@ -40,6 +40,7 @@ def parse():
     p.add_argument("--seed", type=int, default=20251015)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--bvh2", action="store_true", help="force the reference BVH2 walk (A/B)")
     p.add_argument("--max-paths", type=int, default=0, help="paths per wavefront chunk (0 = library default)")
     return p.parse_args()
 
@@ -90,10 +91,12 @@ def main():
         else:
             rt.synchronize()
 
+    base = N.RTG_OPT_CULL | (N.RTG_OPT_BVH2 if a.bvh2 else 0)
+    rt.set_options(flags=base)
     for _ in range(a.warmup):
         step()
     # timed region: per-launch HIP events on the render stream give the closest-hit kernel time
-    rt.set_options(flags=N.RTG_OPT_CULL | N.RTG_OPT_TIMING)
+    rt.set_options(flags=base | N.RTG_OPT_TIMING)
     ext_rays = shadow_rays = paths = 0
     extend_ms = shadow_ms = shade_ms = 0.0
     extend_launches = 0
@@ -111,18 +114,22 @@ def main():
         extend_launches += st["extend_launches"]
     barrier_sync()
     elapsed = time.perf_counter() - t_start
-    rt.set_options(flags=N.RTG_OPT_CULL)
 
-    # counting pass (untimed): box / triangle tests per closest-hit ray on the same workload
-    rt.set_options(flags=N.RTG_OPT_CULL | N.RTG_OPT_COUNT)
-    rt.clear()
-    rt.render(a.spp, tiles=tiles, first_sample=0)
-    cs = rt.stats()
-    rt.set_options(flags=N.RTG_OPT_CULL)
+    # counting passes (untimed): box / triangle tests per closest-hit ray on the same workload.
+    # Algorithmic work is the reference's BVH2 walk; the 4-wide walk's own tests are reported too.
+    def count(flags):
+        rt.set_options(flags=flags | N.RTG_OPT_COUNT)
+        rt.clear()
+        rt.render(a.spp, tiles=tiles, first_sample=0)
+        return rt.stats()
+    cs = count(N.RTG_OPT_CULL | N.RTG_OPT_BVH2)
+    cw = cs if a.bvh2 else count(base)
+    rt.set_options(flags=base)
 
     local_kernel_ms = (extend_ms, shadow_ms, shade_ms)
     totals = np.array([ext_rays, shadow_rays, paths, extend_ms, extend_launches,
-                       cs["node_visits"], cs["tri_tests"], cs["extension_rays"]], dtype=np.float64)
+                       cs["node_visits"], cs["tri_tests"], cs["extension_rays"],
+                       cw["node_visits"], cw["tri_tests"]], dtype=np.float64)
     t_max = elapsed
     if world > 1:
         import torch
@@ -132,7 +139,7 @@ def main():
         te = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         t_max = float(te.item())
-    ext_rays, shadow_rays, paths, extend_ms, extend_launches, c_nodes, c_tris, c_ext = totals.tolist()
+    ext_rays, shadow_rays, paths, extend_ms, extend_launches, c_nodes, c_tris, c_ext, w_nodes, w_tris = totals.tolist()
     rays = ext_rays + shadow_rays
     mrays = rays / t_max / 1e6
     ms_step = t_max * 1e3 / a.steps
@@ -182,6 +189,9 @@ def main():
                          "traffic": traffic,
                          "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
                          "tri_tests_per_ray": round(tris_per_ray, 2),
+                         "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from the reference BVH2)",
+                         "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
+                         "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
                          "avg_launch_ms": round(extend_ms / max(extend_launches, 1), 4)},
             "kernel_ms_per_step_rank0": {"closest_hit": round(local_kernel_ms[0] / a.steps, 2),
                                          "any_hit": round(local_kernel_ms[1] / a.steps, 2),

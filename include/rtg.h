@@ -116,11 +116,13 @@ void rtg_destroy(rtg_handle* h);
  * most max_depth+2 closest-hit segments. flags: RTG_OPT_CULL enables the conservative distance
  * culling (without it traversal visits exactly the reference's node set: verification mode);
  * RTG_OPT_COUNT runs the counting kernels (node / triangle tests in rtg_stats);
- * RTG_OPT_TIMING records HIP events around every launch (per-kernel-class ms in rtg_stats).
+ * RTG_OPT_TIMING records HIP events around every launch (per-kernel-class ms in rtg_stats);
+ * RTG_OPT_BVH2 forces the reference BVH2 walk (no 4-wide collapse; verification / A-B).
  * max_paths_in_flight bounds the paths of one wavefront chunk (0 = keep, default 64M). */
 #define RTG_OPT_CULL   1
 #define RTG_OPT_COUNT  2
 #define RTG_OPT_TIMING 4
+#define RTG_OPT_BVH2   8
 int  rtg_set_options(rtg_handle* h, int max_depth, int flags, uint32_t max_paths_in_flight);
 
 /* Add samples [first_sample, first_sample+n_samples) of every pixel in the listed 32x32 tiles

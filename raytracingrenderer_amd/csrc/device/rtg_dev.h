@@ -83,6 +83,15 @@ struct __align__(16) DevNode {
     float4 c;  // rmin.z rmax.x rmax.y rmax.z
     int4 d;    // left word, right word, -, -
 };
+// 4-wide node collapsed from the reference BVH2 (slots = grandchildren, or a leaf child), one
+// 128-byte line: slot k's box in component k of each plane. Empty slot: word = RTG_EXIT.
+struct __align__(16) DevNode4 {
+    float4 mnx, mny, mnz, mxx, mxy, mxz;
+    int4 w;
+    int4 pad;
+};
+RTG_D float comp4(const float4& v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w)); }
+RTG_D int comp4i(const int4& v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w)); }
 // Hot intersection record (64 B): exactly the operands of Triangle::rayIntersect.
 struct __align__(16) DevTri {
     float4 nd;    // n.xyz, d
@@ -119,6 +128,7 @@ struct DevCamera {
 
 struct SceneView {
     const DevNode* nodes;
+    const DevNode4* nodes4;  // collapsed 4-wide tree (exact for rays with finite 1/d)
     const DevTri* tris;
     const DevShade* shade;
     const DevMat* mats;
@@ -128,6 +138,8 @@ struct SceneView {
     int n_lights;
     int env_tex;         // -1: BackgroundColour(0)
     int root_word;       // child word of the root (RTG_EXIT if no triangles)
+    int root_word4;      // root word in the 4-wide tree
+    int use4;            // 4-wide tree available (all bounds finite)
     float root_box[6];   // bounds of the reference root node
     float cull_scale;    // scene magnitude used for the conservative cull inflation
 };

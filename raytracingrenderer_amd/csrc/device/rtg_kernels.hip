@@ -58,6 +58,7 @@ struct TraceIO {
     int* ovf;                  // global stack overflow [level][thread]
     unsigned long long* stats; // [0,1] closest / [4,5] any-hit: box tests, triangle tests (COUNT)
     int cull;
+    int wide;                  // traverse the 4-wide tree when the ray allows it
 };
 
 struct ChunkArgs {
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tbest = 0.0f, omag = 0.0f, dmag = 0.0f, delta = 0.0f, bu = 0.0f, bv = 0.0f;
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0;
-    bool occluded = false;
+    bool occluded = false, mode4 = false;
     for (;;) {
         // ---- retire finished rays
         if (have && cur == RTG_EXIT) {
@@ -156,8 +157,13 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
                     bu = bv = 0.0f;
                     occluded = false;
                     sp = 0;
+                    // 4-wide only when every 1/d component is finite (no NaN slab terms): then a
+                    // passing grandchild box implies its (skipped) parent box passes.
+                    mode4 = io.wide && s.use4 && fabsf(inv.x) <= RTG_FLT_MAX && fabsf(inv.y) <= RTG_FLT_MAX &&
+                            fabsf(inv.z) <= RTG_FLT_MAX && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
                     const float* rb = s.root_box;
-                    cur = slab_exact(rb[0], rb[1], rb[2], rb[3], rb[4], rb[5], o, inv) ? s.root_word : RTG_EXIT;
+                    cur = slab_exact(rb[0], rb[1], rb[2], rb[3], rb[4], rb[5], o, inv)
+                              ? (mode4 ? s.root_word4 : s.root_word) : RTG_EXIT;
                 }
                 pool_base += take;
                 pool_left -= take;
@@ -166,7 +172,52 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
         if (drained && __ballot(have) == 0) break;
         if (!have || cur == RTG_EXIT) continue;
         // ---- one traversal step
-        if (cur >= 0) {
+        if (cur >= 0 && mode4) {
+            const DevNode4 nd = s.nodes4[cur];
+            float key[4];
+            int wd[4];
+            int nh = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int wk = comp4i(nd.w, k);
+                const float mnx = comp4(nd.mnx, k), mny = comp4(nd.mny, k), mnz = comp4(nd.mnz, k);
+                const float mxx = comp4(nd.mxx, k), mxy = comp4(nd.mxy, k), mxz = comp4(nd.mxz, k);
+                bool hit = wk != RTG_EXIT && slab_exact(mnx, mny, mnz, mxx, mxy, mxz, o, inv);
+                const float e = slab_cull_entry(mnx, mny, mnz, mxx, mxy, mxz, o, inv, delta);
+                if (io.cull) hit = hit && !(e > tbest);
+                if (COUNT) c_nodes += wk != RTG_EXIT ? 1 : 0;
+                key[k] = hit ? fmaxf(e, -RTG_FLT_MAX) : __builtin_inff();
+                wd[k] = wk;
+                nh += hit ? 1 : 0;
+            }
+#define RTG_CSWAP(i, j)                                               \
+    if (key[j] < key[i]) {                                           \
+        const float tk = key[i]; key[i] = key[j]; key[j] = tk;      \
+        const int tw = wd[i]; wd[i] = wd[j]; wd[j] = tw;             \
+    }
+            RTG_CSWAP(0, 1) RTG_CSWAP(2, 3) RTG_CSWAP(0, 2) RTG_CSWAP(1, 3) RTG_CSWAP(1, 2)
+#undef RTG_CSWAP
+            if (nh == 0) {
+                if (sp == 0) {
+                    cur = RTG_EXIT;
+                } else {
+                    --sp;
+                    cur = sp < RTG_STACK ? stk[sp][tid] : io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
+                }
+            } else {
+#define RTG_PUSH(w)                                                                  \
+    {                                                                               \
+        if (sp < RTG_STACK) stk[sp][tid] = (w);                                     \
+        else io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid] = (w);              \
+        ++sp;                                                                       \
+    }
+                if (nh > 3) RTG_PUSH(wd[3])
+                if (nh > 2) RTG_PUSH(wd[2])
+                if (nh > 1) RTG_PUSH(wd[1])
+#undef RTG_PUSH
+                cur = wd[0];
+            }
+        } else if (cur >= 0) {
             if (COUNT) c_nodes += 2;
             const DevNode nd = s.nodes[cur];
             bool hl = slab_exact(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, o, inv);
@@ -518,6 +569,8 @@ struct rtg_handle {
     SceneView sv{};
     DevCamera cam{};
     DevNode* d_nodes = nullptr;
+    DevNode4* d_nodes4 = nullptr;
+    int use4 = 0, wide = 1;
     DevTri* d_tris = nullptr;
     DevShade* d_shade = nullptr;
     DevMat* d_mats = nullptr;
@@ -577,7 +630,9 @@ static int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
 
 static int ensure_ovf(rtg_handle* h) {
     int grid = std::max(h->trace_blocks, h->trace_blocks_count);
-    size_t levels = h->bvh_depth + 2 > RTG_STACK ? (size_t)(h->bvh_depth + 2 - RTG_STACK) : 1;
+    // deepest stack: one entry per BVH2 level, or up to 3 per 4-wide level (two BVH2 levels)
+    size_t deep = std::max<size_t>(h->bvh_depth, 3 * ((size_t)h->bvh_depth + 1) / 2) + 2;
+    size_t levels = deep > RTG_STACK ? deep - RTG_STACK : 1;
     size_t need = levels * (size_t)grid * RTG_TB;
     if (need <= h->cap_ovf) return RTG_OK;
     (void)hipFree(h->d_ovf);
@@ -704,6 +759,70 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     if (nt > 0) {
         if (!word(0, root_word)) { g_err = "bad BVH root"; return RTG_ERR_ARG; }
     }
+    // ---- 4-wide collapse: each node's slots are its children's children (a leaf child stays a
+    // slot). Exact boxes are kept, so reachability is the reference's (see k_trace).
+    std::vector<DevNode4> nodes4;
+    int root_word4 = root_word;
+    bool finite = true;
+    for (size_t k = 0; k < (size_t)nn * 6; ++k) finite = finite && std::isfinite(d->node_bounds[k]);
+    // Skipping the middle level is exact only if every child box lies inside its parent's (true for
+    // Scene::build's bounds; checked so that a foreign descriptor degrades to the BVH2 walk).
+    for (uint32_t i = 0; finite && i < nn; ++i) {
+        const int32_t* L = d->node_links + (size_t)i * 4;
+        if (L[0] < 0) continue;
+        const float* P = d->node_bounds + (size_t)i * 6;
+        for (int c : {L[0], L[1]}) {
+            const float* Cb = d->node_bounds + (size_t)c * 6;
+            for (int q = 0; q < 3; ++q) finite = finite && Cb[q] >= P[q] && Cb[q + 3] <= P[q + 3];
+        }
+    }
+    if (nt > 0 && finite && d->node_links[0] >= 0) {
+        auto internal = [&](int i) { return d->node_links[(size_t)i * 4] >= 0; };
+        nodes4.emplace_back();
+        root_word4 = 0;
+        std::vector<std::pair<int, int>> work{{0, 0}};
+        while (!work.empty()) {
+            auto [n2, n4] = work.back();
+            work.pop_back();
+            const int32_t* L = d->node_links + (size_t)n2 * 4;
+            int slots[4], ns = 0;
+            for (int c : {L[0], L[1]}) {
+                if (internal(c)) {
+                    slots[ns++] = d->node_links[(size_t)c * 4 + 0];
+                    slots[ns++] = d->node_links[(size_t)c * 4 + 1];
+                } else {
+                    slots[ns++] = c;
+                }
+            }
+            float plane[6][4];
+            int wd[4] = {RTG_EXIT, RTG_EXIT, RTG_EXIT, RTG_EXIT};
+            for (int k = 0; k < 4; ++k)
+                for (int q = 0; q < 6; ++q) plane[q][k] = 0.0f;
+            for (int k = 0; k < ns; ++k) {
+                const float* bb = d->node_bounds + (size_t)slots[k] * 6;
+                for (int q = 0; q < 6; ++q) plane[q][k] = bb[q];
+                if (internal(slots[k])) {
+                    wd[k] = (int)nodes4.size();
+                    nodes4.emplace_back();
+                    work.push_back({slots[k], wd[k]});
+                } else if (!word(slots[k], wd[k])) {
+                    g_err = "bad BVH leaf";
+                    return RTG_ERR_ARG;
+                }
+            }
+            DevNode4 dn;
+            dn.mnx = make_float4(plane[0][0], plane[0][1], plane[0][2], plane[0][3]);
+            dn.mny = make_float4(plane[1][0], plane[1][1], plane[1][2], plane[1][3]);
+            dn.mnz = make_float4(plane[2][0], plane[2][1], plane[2][2], plane[2][3]);
+            dn.mxx = make_float4(plane[3][0], plane[3][1], plane[3][2], plane[3][3]);
+            dn.mxy = make_float4(plane[4][0], plane[4][1], plane[4][2], plane[4][3]);
+            dn.mxz = make_float4(plane[5][0], plane[5][1], plane[5][2], plane[5][3]);
+            dn.w = make_int4(wd[0], wd[1], wd[2], wd[3]);
+            dn.pad = make_int4(0, 0, 0, 0);
+            nodes4[n4] = dn;
+        }
+    }
+    h->use4 = finite && nt > 0;
     float scale = 0.0f;
     for (int k = 0; k < 6; ++k) {
         float v = std::fabs(d->node_bounds[k]);
@@ -753,6 +872,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     }
     int rc;
     if ((rc = dev_upload(&h->d_nodes, nodes))) return rc;
+    if ((rc = dev_upload(&h->d_nodes4, nodes4))) return rc;
     if ((rc = dev_upload(&h->d_tris, tris))) return rc;
     if ((rc = dev_upload(&h->d_shade, shade))) return rc;
     if ((rc = dev_upload(&h->d_mats, mats))) return rc;
@@ -771,6 +891,9 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     s.n_lights = (int)d->n_lights;
     s.env_tex = d->env_texture;
     s.root_word = root_word;
+    s.nodes4 = h->d_nodes4;
+    s.root_word4 = root_word4;
+    s.use4 = h->use4 ? 1 : 0;
     for (int k = 0; k < 6; ++k) s.root_box[k] = d->node_bounds[k];
     s.cull_scale = scale;
 
@@ -823,7 +946,7 @@ void rtg_destroy(rtg_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_chunk(h);
-    (void)hipFree(h->d_nodes); (void)hipFree(h->d_tris); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
+    (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodes4); (void)hipFree(h->d_tris); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
     (void)hipFree(h->d_lights); (void)hipFree(h->d_texinfo); (void)hipFree(h->d_texels); (void)hipFree(h->d_film);
     (void)hipFree(h->d_pix); (void)hipFree(h->d_ovf); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
     for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
@@ -838,6 +961,7 @@ int rtg_set_options(rtg_handle* h, int max_depth, int cull, uint32_t max_paths) 
     h->cull = cull & 1;
     h->count = (cull >> 1) & 1;   // bit 1: counting kernels (node/triangle tests)
     h->timing = (cull >> 2) & 1;  // bit 2: per-launch timing events
+    h->wide = ((cull >> 3) & 1) ? 0 : 1;  // bit 3: force the reference BVH2 walk
     if (max_paths) h->max_paths = max_paths;
     return RTG_OK;
 }
@@ -912,6 +1036,7 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
     io.ovf = h->d_ovf;
     io.stats = h->d_stats;
     io.cull = h->cull;
+    io.wide = h->wide;
     for (uint32_t s0 = first; s0 < first + n_samples; s0 += ns_chunk) {
         ChunkArgs a;
         a.pixlist = h->d_pix;
@@ -1091,6 +1216,7 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
     io.ovf = h->d_ovf;
     io.stats = h->d_stats;
     io.cull = h->cull;
+    io.wide = h->wide;
     io.queue = d_q;
     io.ray_o = d_o;
     io.ray_d = d_d;

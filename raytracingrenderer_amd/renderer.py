@@ -137,7 +137,7 @@ class RayTracer:
 
     MAX_DEPTH = 4  # Renderer.h:20
 
-    def __init__(self, scene, device=0, max_depth=MAX_DEPTH, seed=1234, cull=True, max_paths=0):
+    def __init__(self, scene, device=0, max_depth=MAX_DEPTH, seed=1234, cull=True, max_paths=0, wide=True):
         self.scene = scene
         self.seed = seed
         self._lib = N.rtg()
@@ -146,7 +146,7 @@ class RayTracer:
         self._h = h
         self.width, self.height = scene.width, scene.height
         self.max_depth = max_depth
-        self.flags = N.RTG_OPT_CULL if cull else 0
+        self.flags = (N.RTG_OPT_CULL if cull else 0) | (0 if wide else N.RTG_OPT_BVH2)
         self.set_options(max_depth=max_depth, flags=self.flags, max_paths=max_paths)
 
     def __del__(self):

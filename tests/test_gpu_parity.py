@@ -27,8 +27,8 @@ def assert_bitexact(got, want, what=""):
                              % (what, len(diff), diff[0].tolist(), got[tuple(diff[0])], want[tuple(diff[0])]))
 
 
-def gpu_film(scene, spp, seed=1234, max_depth=4, cull=True, max_paths=0, tiles=None):
-    rt = RayTracer(scene, seed=seed, max_depth=max_depth, cull=cull, max_paths=max_paths)
+def gpu_film(scene, spp, seed=1234, max_depth=4, cull=True, max_paths=0, tiles=None, wide=True):
+    rt = RayTracer(scene, seed=seed, max_depth=max_depth, cull=cull, max_paths=max_paths, wide=wide)
     rt.render(spp, tiles=tiles, first_sample=0)
     film, n = rt.film()
     assert n == spp
@@ -58,6 +58,26 @@ def test_c1_bit_exact_and_known_answer(cornell256):
 def test_cull_is_exact(cornell256, synth20k):
     for s, spp in ((cornell256, 2), (synth20k, 2)):
         assert_bitexact(gpu_film(s, spp, cull=True), gpu_film(s, spp, cull=False), "cull vs no-cull")
+
+
+def test_wide_walk_is_exact(cornell256, synth20k):
+    """The 4-wide walk (collapsed BVH) returns the reference BVH2 walk's results bit for bit."""
+    for s, spp in ((cornell256, 2), (synth20k, 2)):
+        assert_bitexact(gpu_film(s, spp, wide=True), gpu_film(s, spp, wide=False), "bvh4 vs bvh2 film")
+    rng = np.random.default_rng(11)
+    n = 200000
+    r = np.zeros((n, 8), np.float32)
+    r[:, :3] = rng.uniform(-1.3, 1.3, (n, 3))
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[: n // 10, rng.integers(0, 3)] = 0.0  # some rays stay on the BVH2 walk (inf 1/d)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    r[:, 4:7] = d
+    r[:, 3] = rng.uniform(0.01, 3, n)
+    for cull in (True, False):
+        a = RayTracer(synth20k, cull=cull, wide=True)
+        b = RayTracer(synth20k, cull=cull, wide=False)
+        assert_bitexact(a.trace_closest(r), b.trace_closest(r), "bvh4 vs bvh2 closest")
+        assert np.array_equal(a.trace_visible(r), b.trace_visible(r))
 
 
 @pytest.mark.parametrize("max_depth", [0, 1, 8, 16])
