@@ -192,6 +192,8 @@ def main():
                          "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from the reference BVH2)",
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
+                         "lane_util_node_leaf": [round(cw["node_lane_steps"] / max(cw["lane_slots"], 1), 3),
+                                                 round(cw["leaf_lane_steps"] / max(cw["lane_slots"], 1), 3)],
                          "avg_launch_ms": round(extend_ms / max(extend_launches, 1), 4)},
             "kernel_ms_per_step_rank0": {"closest_hit": round(local_kernel_ms[0] / a.steps, 2),
                                          "any_hit": round(local_kernel_ms[1] / a.steps, 2),

@@ -100,6 +100,9 @@ typedef struct rtg_stats {
     double   extend_ms;            /* RTG_OPT_TIMING: closest-hit kernel time (last call)      */
     double   shadow_ms;            /* device time spent in any-hit kernels (last call)         */
     double   shade_ms;             /* device time spent in generate/shade/accumulate kernels   */
+    uint64_t lane_slots;           /* RTG_OPT_COUNT: closest-hit loop iterations x 64 lanes     */
+    uint64_t node_lane_steps;      /* RTG_OPT_COUNT: lanes doing a node step, summed            */
+    uint64_t leaf_lane_steps;      /* RTG_OPT_COUNT: lanes doing a leaf step, summed            */
 } rtg_stats;
 
 typedef struct rtg_handle rtg_handle;

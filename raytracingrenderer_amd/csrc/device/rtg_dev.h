@@ -83,15 +83,35 @@ struct __align__(16) DevNode {
     float4 c;  // rmin.z rmax.x rmax.y rmax.z
     int4 d;    // left word, right word, -, -
 };
-// 4-wide node collapsed from the reference BVH2 (slots = grandchildren, or a leaf child), one
-// 128-byte line: slot k's box in component k of each plane. Empty slot: word = RTG_EXIT.
-struct __align__(16) DevNode4 {
-    float4 mnx, mny, mnz, mxx, mxy, mxz;
-    int4 w;
-    int4 pad;
+// Wide node collapsed from the reference BVH2: its slots are a cut of the BVH2 subtree (leaves stay
+// slots). RTG_WIDTH*32 bytes: six planes of RTG_WIDTH floats (min x,y,z, max x,y,z; slot k's box in
+// element k), RTG_WIDTH child words (RTG_EXIT = empty slot), RTG_WIDTH pad words.
+#ifndef RTG_WIDTH
+#define RTG_WIDTH 4
+#endif
+#define RTG_WQ (RTG_WIDTH / 4)         // float4s per plane
+#define RTG_WNODE_F4 (RTG_WIDTH * 2)   // float4s per node
+struct __align__(16) DevNodeW {
+    float4 q[RTG_WNODE_F4];
 };
-RTG_D float comp4(const float4& v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w)); }
-RTG_D int comp4i(const int4& v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w)); }
+// Compressed 4-wide node (64 B). Slot boxes are stored conservatively: 8-bit offsets from the
+// node's min corner in power-of-two steps, rounded outward and checked on the host with the
+// device's own decode arithmetic, so a decoded box always contains the exact one. Exactness then
+// rests on the leaf: a candidate hit counts only if its reference leaf box passes the exact slab
+// test (leafbox, per triangle), which by containment also implies every ancestor's.
+//   q[0] = origin.xyz, biased exponents (x | y<<8 | z<<16)
+//   q[1] = planes min x, min y, min z, max x  (byte k = slot k)
+//   q[2] = planes max y, max z, child words 0, 1
+//   q[3] = child words 2, 3, -, -
+#ifndef RTG_QNODE
+#define RTG_QNODE 1
+#endif
+struct __align__(16) DevNodeQ {
+    float4 q[4];
+};
+__host__ __device__ inline float qdecode(float origin, unsigned plane, int k, float scale) {
+    return origin + (float)((plane >> (8 * k)) & 255u) * scale;
+}
 // Hot intersection record (64 B): exactly the operands of Triangle::rayIntersect.
 struct __align__(16) DevTri {
     float4 nd;    // n.xyz, d
@@ -128,7 +148,9 @@ struct DevCamera {
 
 struct SceneView {
     const DevNode* nodes;
-    const DevNode4* nodes4;  // collapsed 4-wide tree (exact for rays with finite 1/d)
+    const DevNodeW* nodesw;  // collapsed wide tree (exact for rays with finite nonzero 1/d)
+    const DevNodeQ* nodesq;  // compressed 4-wide tree (RTG_QNODE)
+    const float4* leafbox;   // [2 per triangle] exact box of the reference leaf holding it
     const DevTri* tris;
     const DevShade* shade;
     const DevMat* mats;
@@ -138,8 +160,8 @@ struct SceneView {
     int n_lights;
     int env_tex;         // -1: BackgroundColour(0)
     int root_word;       // child word of the root (RTG_EXIT if no triangles)
-    int root_word4;      // root word in the 4-wide tree
-    int use4;            // 4-wide tree available (all bounds finite)
+    int root_wordw;      // root word in the wide tree
+    int usew;            // wide tree available (finite bounds, children inside parents)
     float root_box[6];   // bounds of the reference root node
     float cull_scale;    // scene magnitude used for the conservative cull inflation
 };

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -35,7 +36,13 @@
 using namespace rtgd;
 
 #define RTG_TB 256          // threads per block (4 waves)
+#define RTG_POP ((int)0x80000001)  // "pop the stack" marker inside one traversal step
+#ifndef RTG_STACK
 #define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (24 KB per block)
+#endif
+#ifndef RTG_TRACE_WPE
+#define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel
+#endif
 #define RTG_CULL_REL 1.52587890625e-05f  // 2^-16 relative inflation for distance culling
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 4                // min waves per SIMD for k_shade (register budget)
@@ -97,14 +104,15 @@ static __device__ __forceinline__ unsigned prefix_lt(unsigned long long m) {
 // immediately takes the next index from the pool. Without replacement a wave runs until its
 // longest ray finishes (measured SIMD efficiency ~27 %).
 template <bool ANY, bool COUNT>
-__global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
+__global__ __launch_bounds__(RTG_TB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
+void k_trace(SceneView s, TraceIO io) {
     __shared__ int stk[RTG_STACK][RTG_TB];
     const int tid = threadIdx.x;
     const int lane = lane_id();
     const unsigned gthreads = gridDim.x * blockDim.x;
     const unsigned gtid = blockIdx.x * blockDim.x + tid;
     const unsigned n = *io.count;
-    unsigned long long c_nodes = 0, c_tris = 0;
+    unsigned long long c_nodes = 0, c_tris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0;
     unsigned pool_base = 0, pool_left = 0;  // wave-uniform
     bool drained = false;                   // wave-uniform
     bool have = false;
@@ -112,7 +120,7 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tbest = 0.0f, omag = 0.0f, dmag = 0.0f, delta = 0.0f, bu = 0.0f, bv = 0.0f;
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0;
-    bool occluded = false, mode4 = false;
+    bool occluded = false, wide = false;
     for (;;) {
         // ---- retire finished rays
         if (have && cur == RTG_EXIT) {
@@ -157,64 +165,113 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
                     bu = bv = 0.0f;
                     occluded = false;
                     sp = 0;
-                    // 4-wide only when every 1/d component is finite (no NaN slab terms): then a
-                    // passing grandchild box implies its (skipped) parent box passes.
-                    mode4 = io.wide && s.use4 && fabsf(inv.x) <= RTG_FLT_MAX && fabsf(inv.y) <= RTG_FLT_MAX &&
+                    // Wide walk only when every 1/d component is finite and nonzero (no NaN slab
+                    // terms): then a passing descendant box implies its skipped ancestors pass.
+                    wide = io.wide && s.usew && fabsf(inv.x) <= RTG_FLT_MAX && fabsf(inv.y) <= RTG_FLT_MAX &&
                             fabsf(inv.z) <= RTG_FLT_MAX && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
                     const float* rb = s.root_box;
                     cur = slab_exact(rb[0], rb[1], rb[2], rb[3], rb[4], rb[5], o, inv)
-                              ? (mode4 ? s.root_word4 : s.root_word) : RTG_EXIT;
+                              ? (wide ? s.root_wordw : s.root_word) : RTG_EXIT;
                 }
                 pool_base += take;
                 pool_left -= take;
             }
         }
         if (drained && __ballot(have) == 0) break;
+        if (COUNT && !ANY) {
+            c_slots += 64;
+            c_nstep += (have && cur >= 0) ? 1 : 0;
+            c_lstep += (have && cur != RTG_EXIT && cur < 0) ? 1 : 0;
+        }
         if (!have || cur == RTG_EXIT) continue;
         // ---- one traversal step
-        if (cur >= 0 && mode4) {
-            const DevNode4 nd = s.nodes4[cur];
-            float key[4];
-            int wd[4];
+        if (cur >= 0 && wide) {
+            float pl[6][RTG_WIDTH];
+            int wd[RTG_WIDTH];
+            float key[RTG_WIDTH];
+#if RTG_QNODE
+            {
+                const float4* np = s.nodesq[cur].q;
+                const float4 h0 = np[0], h1 = np[1], h2 = np[2], h3 = np[3];
+                const unsigned ex = __float_as_uint(h0.w);
+                const float sx = __uint_as_float((ex & 255u) << 23);
+                const float sy = __uint_as_float(((ex >> 8) & 255u) << 23);
+                const float sz = __uint_as_float(((ex >> 16) & 255u) << 23);
+                const unsigned p0 = __float_as_uint(h1.x), p1 = __float_as_uint(h1.y), p2 = __float_as_uint(h1.z);
+                const unsigned p3 = __float_as_uint(h1.w), p4 = __float_as_uint(h2.x), p5 = __float_as_uint(h2.y);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    pl[0][k] = qdecode(h0.x, p0, k, sx);
+                    pl[1][k] = qdecode(h0.y, p1, k, sy);
+                    pl[2][k] = qdecode(h0.z, p2, k, sz);
+                    pl[3][k] = qdecode(h0.x, p3, k, sx);
+                    pl[4][k] = qdecode(h0.y, p4, k, sy);
+                    pl[5][k] = qdecode(h0.z, p5, k, sz);
+                }
+                wd[0] = __float_as_int(h2.z);
+                wd[1] = __float_as_int(h2.w);
+                wd[2] = __float_as_int(h3.x);
+                wd[3] = __float_as_int(h3.y);
+            }
+#else
+            const float4* np = s.nodesw[cur].q;
+#pragma unroll
+            for (int q = 0; q < 6 * RTG_WQ; ++q) {
+                const float4 v = np[q];
+                pl[q / RTG_WQ][(q % RTG_WQ) * 4 + 0] = v.x;
+                pl[q / RTG_WQ][(q % RTG_WQ) * 4 + 1] = v.y;
+                pl[q / RTG_WQ][(q % RTG_WQ) * 4 + 2] = v.z;
+                pl[q / RTG_WQ][(q % RTG_WQ) * 4 + 3] = v.w;
+            }
+#pragma unroll
+            for (int q = 0; q < RTG_WQ; ++q) {
+                const float4 v = np[6 * RTG_WQ + q];
+                wd[q * 4 + 0] = __float_as_int(v.x);
+                wd[q * 4 + 1] = __float_as_int(v.y);
+                wd[q * 4 + 2] = __float_as_int(v.z);
+                wd[q * 4 + 3] = __float_as_int(v.w);
+            }
+#endif
             int nh = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int wk = comp4i(nd.w, k);
-                const float mnx = comp4(nd.mnx, k), mny = comp4(nd.mny, k), mnz = comp4(nd.mnz, k);
-                const float mxx = comp4(nd.mxx, k), mxy = comp4(nd.mxy, k), mxz = comp4(nd.mxz, k);
-                bool hit = wk != RTG_EXIT && slab_exact(mnx, mny, mnz, mxx, mxy, mxz, o, inv);
+            for (int k = 0; k < RTG_WIDTH; ++k) {
+                const float mnx = pl[0][k], mny = pl[1][k], mnz = pl[2][k];
+                const float mxx = pl[3][k], mxy = pl[4][k], mxz = pl[5][k];
+                bool hit = wd[k] != RTG_EXIT && slab_exact(mnx, mny, mnz, mxx, mxy, mxz, o, inv);
                 const float e = slab_cull_entry(mnx, mny, mnz, mxx, mxy, mxz, o, inv, delta);
                 if (io.cull) hit = hit && !(e > tbest);
-                if (COUNT) c_nodes += wk != RTG_EXIT ? 1 : 0;
+                if (COUNT) c_nodes += wd[k] != RTG_EXIT ? 1 : 0;
                 key[k] = hit ? fmaxf(e, -RTG_FLT_MAX) : __builtin_inff();
-                wd[k] = wk;
                 nh += hit ? 1 : 0;
             }
+            // ascending entry distance (misses sort last); order only affects culling, not results
 #define RTG_CSWAP(i, j)                                               \
     if (key[j] < key[i]) {                                           \
         const float tk = key[i]; key[i] = key[j]; key[j] = tk;      \
         const int tw = wd[i]; wd[i] = wd[j]; wd[j] = tw;             \
     }
+#if RTG_WIDTH == 4
             RTG_CSWAP(0, 1) RTG_CSWAP(2, 3) RTG_CSWAP(0, 2) RTG_CSWAP(1, 3) RTG_CSWAP(1, 2)
+#else
+            RTG_CSWAP(0, 1) RTG_CSWAP(2, 3) RTG_CSWAP(4, 5) RTG_CSWAP(6, 7)
+            RTG_CSWAP(0, 2) RTG_CSWAP(1, 3) RTG_CSWAP(4, 6) RTG_CSWAP(5, 7)
+            RTG_CSWAP(1, 2) RTG_CSWAP(5, 6)
+            RTG_CSWAP(0, 4) RTG_CSWAP(1, 5) RTG_CSWAP(2, 6) RTG_CSWAP(3, 7)
+            RTG_CSWAP(2, 4) RTG_CSWAP(3, 5)
+            RTG_CSWAP(1, 2) RTG_CSWAP(3, 4) RTG_CSWAP(5, 6)
+#endif
 #undef RTG_CSWAP
             if (nh == 0) {
-                if (sp == 0) {
-                    cur = RTG_EXIT;
-                } else {
-                    --sp;
-                    cur = sp < RTG_STACK ? stk[sp][tid] : io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
-                }
+                cur = RTG_POP;
             } else {
-#define RTG_PUSH(w)                                                                  \
-    {                                                                               \
-        if (sp < RTG_STACK) stk[sp][tid] = (w);                                     \
-        else io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid] = (w);              \
-        ++sp;                                                                       \
-    }
-                if (nh > 3) RTG_PUSH(wd[3])
-                if (nh > 2) RTG_PUSH(wd[2])
-                if (nh > 1) RTG_PUSH(wd[1])
-#undef RTG_PUSH
+#pragma unroll
+                for (int k = RTG_WIDTH - 1; k >= 1; --k) {
+                    if (k < nh) {
+                        if (sp < RTG_STACK) stk[sp][tid] = wd[k];
+                        else io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid] = wd[k];
+                        ++sp;
+                    }
+                }
                 cur = wd[0];
             }
         } else if (cur >= 0) {
@@ -240,25 +297,36 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
                 cur = nd.d.x;
             } else if (hr) {
                 cur = nd.d.y;
-            } else if (sp == 0) {
-                cur = RTG_EXIT;
             } else {
-                --sp;
-                cur = sp < RTG_STACK ? stk[sp][tid] : io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
+                cur = RTG_POP;
             }
         } else {
             const int code = ~cur;
             const int start = code >> 1;
             const int cnt = (code & 1) + 1;
+            bool lchk = false, lok = true;  // exact leaf box, tested on the first candidate only
             for (int k = 0; k < cnt; ++k) {
                 const int tri = start + k;
                 if (COUNT) c_tris += 1;
                 const DevTri T = s.tris[tri];
                 float t, u, v;
                 if (tri_intersect(T, o, d, t, u, v)) {
-                    if (ANY) {
-                        if (!(t >= tbest || t <= RTG_EPS)) occluded = true;
-                    } else if (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid))) {
+                    bool cand = ANY ? !(t >= tbest || t <= RTG_EPS)
+                                    : (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid)));
+#if RTG_QNODE
+                    if (cand && wide) {
+                        if (!lchk) {
+                            const float4 b0 = s.leafbox[2 * start], b1 = s.leafbox[2 * start + 1];
+                            lok = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
+                            lchk = true;
+                        }
+                        cand = lok;
+                    }
+#endif
+                    if (!cand) {
+                    } else if (ANY) {
+                        occluded = true;
+                    } else {
                         tbest = t;
                         bid = tri;
                         bu = u;
@@ -267,13 +335,17 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
                     }
                 }
             }
-            if (ANY && occluded) {
-                cur = RTG_EXIT;
-            } else if (sp == 0) {
+            cur = (ANY && occluded) ? RTG_EXIT : RTG_POP;
+        }
+        // ---- one pop for every branch: always an LDS read (ds_read, not a flat load through a
+        // selected pointer); the global overflow read only for deep entries
+        if (cur == RTG_POP) {
+            if (sp == 0) {
                 cur = RTG_EXIT;
             } else {
                 --sp;
-                cur = sp < RTG_STACK ? stk[sp][tid] : io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
+                cur = stk[sp < RTG_STACK ? sp : 0][tid];
+                if (sp >= RTG_STACK) cur = io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
             }
         }
     }
@@ -281,10 +353,17 @@ __global__ __launch_bounds__(RTG_TB) void k_trace(SceneView s, TraceIO io) {
         for (int off = 32; off > 0; off >>= 1) {
             c_nodes += __shfl_down(c_nodes, off);
             c_tris += __shfl_down(c_tris, off);
+            c_nstep += __shfl_down(c_nstep, off);
+            c_lstep += __shfl_down(c_lstep, off);
         }
         if (lane == 0) {
             atomicAdd(&io.stats[ANY ? 4 : 0], c_nodes);
             atomicAdd(&io.stats[ANY ? 5 : 1], c_tris);
+            if (!ANY) {
+                atomicAdd(&io.stats[8], c_slots);
+                atomicAdd(&io.stats[9], c_nstep);
+                atomicAdd(&io.stats[10], c_lstep);
+            }
         }
     }
 }
@@ -569,8 +648,11 @@ struct rtg_handle {
     SceneView sv{};
     DevCamera cam{};
     DevNode* d_nodes = nullptr;
-    DevNode4* d_nodes4 = nullptr;
-    int use4 = 0, wide = 1;
+    DevNodeW* d_nodesw = nullptr;
+    DevNodeQ* d_nodesq = nullptr;
+    float4* d_leafbox = nullptr;
+    int usew = 0, wide = 1;
+    uint32_t wide_depth = 0;  // wide levels on the longest root-to-leaf path
     DevTri* d_tris = nullptr;
     DevShade* d_shade = nullptr;
     DevMat* d_mats = nullptr;
@@ -630,8 +712,9 @@ static int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
 
 static int ensure_ovf(rtg_handle* h) {
     int grid = std::max(h->trace_blocks, h->trace_blocks_count);
-    // deepest stack: one entry per BVH2 level, or up to 3 per 4-wide level (two BVH2 levels)
-    size_t deep = std::max<size_t>(h->bvh_depth, 3 * ((size_t)h->bvh_depth + 1) / 2) + 2;
+    // deepest stack: one entry per BVH2 level, or up to RTG_WIDTH-1 per wide level (each wide
+    // level descends at least one BVH2 level)
+    size_t deep = std::max<size_t>(h->bvh_depth, (size_t)h->wide_depth * (RTG_WIDTH - 1)) + 2;
     size_t levels = deep > RTG_STACK ? deep - RTG_STACK : 1;
     size_t need = levels * (size_t)grid * RTG_TB;
     if (need <= h->cap_ovf) return RTG_OK;
@@ -642,6 +725,53 @@ static int ensure_ovf(rtg_handle* h) {
 }
 
 static float host_bits_f(int v) { float f; std::memcpy(&f, &v, 4); return f; }
+
+// Compressed 4-wide node: per axis the smallest power-of-two step with origin + 255*step >= max,
+// then each slot bound rounded outward and verified with the device's decode (qdecode), so the
+// decoded box contains the exact one. Returns false if a step would leave the exponent range.
+static bool encode_qnode(const float* bounds, const std::vector<int>& slots, const int32_t* words, DevNodeQ& out) {
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = bounds[(size_t)slots[0] * 6 + a];
+        hi[a] = bounds[(size_t)slots[0] * 6 + 3 + a];
+        for (int k = 1; k < (int)slots.size(); ++k) {
+            lo[a] = std::min(lo[a], bounds[(size_t)slots[k] * 6 + a]);
+            hi[a] = std::max(hi[a], bounds[(size_t)slots[k] * 6 + 3 + a]);
+        }
+    }
+    unsigned planes[6] = {0, 0, 0, 0, 0, 0};
+    unsigned bexp[3];
+    for (int a = 0; a < 3; ++a) {
+        const double ext = (double)hi[a] - (double)lo[a];
+        int e = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -126;
+        e = std::max(e, -126);
+        for (;; ++e) {
+            if (e > 119) return false;
+            if (rtgd::qdecode(lo[a], 255u, 0, host_bits_f((e + 127) << 23)) >= hi[a]) break;
+        }
+        bexp[a] = (unsigned)(e + 127);
+        const float sc = host_bits_f((e + 127) << 23);
+        for (int k = 0; k < (int)slots.size(); ++k) {
+            const float mn = bounds[(size_t)slots[k] * 6 + a], mx = bounds[(size_t)slots[k] * 6 + 3 + a];
+            int ql = (int)std::floor(((double)mn - (double)lo[a]) / std::ldexp(1.0, e));
+            int qh = (int)std::ceil(((double)mx - (double)lo[a]) / std::ldexp(1.0, e));
+            ql = std::min(std::max(ql, 0), 255);
+            qh = std::min(std::max(qh, 0), 255);
+            while (ql > 0 && rtgd::qdecode(lo[a], (unsigned)ql, 0, sc) > mn) --ql;
+            while (qh < 255 && rtgd::qdecode(lo[a], (unsigned)qh, 0, sc) < mx) ++qh;
+            if (rtgd::qdecode(lo[a], (unsigned)ql, 0, sc) > mn || rtgd::qdecode(lo[a], (unsigned)qh, 0, sc) < mx)
+                return false;
+            planes[a] |= (unsigned)ql << (8 * k);
+            planes[3 + a] |= (unsigned)qh << (8 * k);
+        }
+    }
+    auto uf = [](unsigned v) { float f; std::memcpy(&f, &v, 4); return f; };
+    out.q[0] = make_float4(lo[0], lo[1], lo[2], uf(bexp[0] | (bexp[1] << 8) | (bexp[2] << 16)));
+    out.q[1] = make_float4(uf(planes[0]), uf(planes[1]), uf(planes[2]), uf(planes[3]));
+    out.q[2] = make_float4(uf(planes[4]), uf(planes[5]), host_bits_f(words[0]), host_bits_f(words[1]));
+    out.q[3] = make_float4(host_bits_f(words[2]), host_bits_f(words[3]), 0.0f, 0.0f);
+    return true;
+}
 static float host_dot(const float* a, const float* b) { return ((a[0] * b[0]) + (a[1] * b[1])) + (a[2] * b[2]); }
 static void host_cross(const float* a, const float* b, float* o) {
     o[0] = (a[1] * b[2]) - (a[2] * b[1]);
@@ -759,13 +889,16 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     if (nt > 0) {
         if (!word(0, root_word)) { g_err = "bad BVH root"; return RTG_ERR_ARG; }
     }
-    // ---- 4-wide collapse: each node's slots are its children's children (a leaf child stays a
-    // slot). Exact boxes are kept, so reachability is the reference's (see k_trace).
-    std::vector<DevNode4> nodes4;
-    int root_word4 = root_word;
+    // ---- wide collapse: each node's slots are a cut of the BVH2 subtree below it, grown by
+    // repeatedly opening the internal slot of largest surface area (leaves stay slots). Exact
+    // boxes are kept, so reachability is the reference's (see k_trace).
+    std::vector<DevNodeW> nodesw;
+    std::vector<DevNodeQ> nodesq;
+    bool qok = true;
+    int root_wordw = root_word;
     bool finite = true;
     for (size_t k = 0; k < (size_t)nn * 6; ++k) finite = finite && std::isfinite(d->node_bounds[k]);
-    // Skipping the middle level is exact only if every child box lies inside its parent's (true for
+    // Skipping levels is exact only if every child box lies inside its parent's (true for
     // Scene::build's bounds; checked so that a foreign descriptor degrades to the BVH2 walk).
     for (uint32_t i = 0; finite && i < nn; ++i) {
         const int32_t* L = d->node_links + (size_t)i * 4;
@@ -778,51 +911,77 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     }
     if (nt > 0 && finite && d->node_links[0] >= 0) {
         auto internal = [&](int i) { return d->node_links[(size_t)i * 4] >= 0; };
-        nodes4.emplace_back();
-        root_word4 = 0;
-        std::vector<std::pair<int, int>> work{{0, 0}};
+        auto area = [&](int i) {
+            const float* b = d->node_bounds + (size_t)i * 6;
+            const double x = b[3] - b[0], y = b[4] - b[1], z = b[5] - b[2];
+            return x * y + y * z + z * x;
+        };
+        nodesw.emplace_back();
+        nodesq.emplace_back();
+        root_wordw = 0;
+        std::vector<std::array<int, 3>> work{{0, 0, 1}};  // BVH2 node, wide node, wide level
         while (!work.empty()) {
-            auto [n2, n4] = work.back();
+            auto [n2, nw, lvl] = work.back();
             work.pop_back();
-            const int32_t* L = d->node_links + (size_t)n2 * 4;
-            int slots[4], ns = 0;
-            for (int c : {L[0], L[1]}) {
-                if (internal(c)) {
-                    slots[ns++] = d->node_links[(size_t)c * 4 + 0];
-                    slots[ns++] = d->node_links[(size_t)c * 4 + 1];
-                } else {
-                    slots[ns++] = c;
-                }
+            h->wide_depth = std::max(h->wide_depth, (uint32_t)lvl);
+            std::vector<int> slots{d->node_links[(size_t)n2 * 4], d->node_links[(size_t)n2 * 4 + 1]};
+            while ((int)slots.size() < RTG_WIDTH) {
+                int best = -1;
+                for (int k = 0; k < (int)slots.size(); ++k)
+                    if (internal(slots[k]) && (best < 0 || area(slots[k]) > area(slots[best]))) best = k;
+                if (best < 0) break;
+                const int c = slots[best];
+                slots[best] = d->node_links[(size_t)c * 4];
+                slots.push_back(d->node_links[(size_t)c * 4 + 1]);
             }
-            float plane[6][4];
-            int wd[4] = {RTG_EXIT, RTG_EXIT, RTG_EXIT, RTG_EXIT};
-            for (int k = 0; k < 4; ++k)
-                for (int q = 0; q < 6; ++q) plane[q][k] = 0.0f;
-            for (int k = 0; k < ns; ++k) {
-                const float* bb = d->node_bounds + (size_t)slots[k] * 6;
-                for (int q = 0; q < 6; ++q) plane[q][k] = bb[q];
+#if RTG_QNODE
+            int32_t wq[4] = {RTG_EXIT, RTG_EXIT, RTG_EXIT, RTG_EXIT};
+            for (int k = 0; k < (int)slots.size(); ++k) {
                 if (internal(slots[k])) {
-                    wd[k] = (int)nodes4.size();
-                    nodes4.emplace_back();
-                    work.push_back({slots[k], wd[k]});
-                } else if (!word(slots[k], wd[k])) {
+                    wq[k] = (int)nodesq.size();
+                    nodesq.emplace_back();
+                    work.push_back({slots[k], wq[k], lvl + 1});
+                } else if (!word(slots[k], wq[k])) {
                     g_err = "bad BVH leaf";
                     return RTG_ERR_ARG;
                 }
             }
-            DevNode4 dn;
-            dn.mnx = make_float4(plane[0][0], plane[0][1], plane[0][2], plane[0][3]);
-            dn.mny = make_float4(plane[1][0], plane[1][1], plane[1][2], plane[1][3]);
-            dn.mnz = make_float4(plane[2][0], plane[2][1], plane[2][2], plane[2][3]);
-            dn.mxx = make_float4(plane[3][0], plane[3][1], plane[3][2], plane[3][3]);
-            dn.mxy = make_float4(plane[4][0], plane[4][1], plane[4][2], plane[4][3]);
-            dn.mxz = make_float4(plane[5][0], plane[5][1], plane[5][2], plane[5][3]);
-            dn.w = make_int4(wd[0], wd[1], wd[2], wd[3]);
-            dn.pad = make_int4(0, 0, 0, 0);
-            nodes4[n4] = dn;
+            if (!encode_qnode(d->node_bounds, slots, wq, nodesq[nw])) { qok = false; break; }
+            continue;
+#endif
+            float f[RTG_WNODE_F4 * 4];
+            int32_t* wdw = reinterpret_cast<int32_t*>(f + 6 * RTG_WIDTH);
+            for (int k = 0; k < RTG_WNODE_F4 * 4; ++k) f[k] = 0.0f;
+            for (int k = 0; k < RTG_WIDTH; ++k) wdw[k] = RTG_EXIT;
+            for (int k = 0; k < (int)slots.size(); ++k) {
+                const float* bb = d->node_bounds + (size_t)slots[k] * 6;
+                for (int q = 0; q < 6; ++q) f[q * RTG_WIDTH + k] = bb[q];
+                if (internal(slots[k])) {
+                    wdw[k] = (int)nodesw.size();
+                    nodesw.emplace_back();
+                    work.push_back({slots[k], wdw[k], lvl + 1});
+                } else if (!word(slots[k], wdw[k])) {
+                    g_err = "bad BVH leaf";
+                    return RTG_ERR_ARG;
+                }
+            }
+            std::memcpy(&nodesw[nw], f, sizeof(DevNodeW));
         }
     }
-    h->use4 = finite && nt > 0;
+    h->usew = finite && qok && nt > 0;
+    // exact leaf boxes per triangle (compressed walk: candidate hits re-test their leaf)
+    std::vector<float4> leafbox(RTG_QNODE ? std::max<size_t>((size_t)nt * 2, 2) : 2);
+    if (RTG_QNODE) {
+        for (uint32_t i = 0; i < nn; ++i) {
+            const int32_t* L = d->node_links + (size_t)i * 4;
+            if (L[0] >= 0) continue;
+            const float* b = d->node_bounds + (size_t)i * 6;
+            for (int t = L[2]; t < L[3]; ++t) {
+                leafbox[2 * (size_t)t] = make_float4(b[0], b[1], b[2], b[3]);
+                leafbox[2 * (size_t)t + 1] = make_float4(b[4], b[5], 0.0f, 0.0f);
+            }
+        }
+    }
     float scale = 0.0f;
     for (int k = 0; k < 6; ++k) {
         float v = std::fabs(d->node_bounds[k]);
@@ -872,7 +1031,9 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     }
     int rc;
     if ((rc = dev_upload(&h->d_nodes, nodes))) return rc;
-    if ((rc = dev_upload(&h->d_nodes4, nodes4))) return rc;
+    if ((rc = dev_upload(&h->d_nodesw, nodesw))) return rc;
+    if ((rc = dev_upload(&h->d_nodesq, nodesq))) return rc;
+    if ((rc = dev_upload(&h->d_leafbox, leafbox))) return rc;
     if ((rc = dev_upload(&h->d_tris, tris))) return rc;
     if ((rc = dev_upload(&h->d_shade, shade))) return rc;
     if ((rc = dev_upload(&h->d_mats, mats))) return rc;
@@ -891,9 +1052,11 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     s.n_lights = (int)d->n_lights;
     s.env_tex = d->env_texture;
     s.root_word = root_word;
-    s.nodes4 = h->d_nodes4;
-    s.root_word4 = root_word4;
-    s.use4 = h->use4 ? 1 : 0;
+    s.nodesw = h->d_nodesw;
+    s.nodesq = h->d_nodesq;
+    s.leafbox = h->d_leafbox;
+    s.root_wordw = root_wordw;
+    s.usew = h->usew ? 1 : 0;
     for (int k = 0; k < 6; ++k) s.root_box[k] = d->node_bounds[k];
     s.cull_scale = scale;
 
@@ -910,8 +1073,8 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     HIPOK(hipMalloc((void**)&h->d_film, (size_t)h->W * h->H * 3 * sizeof(float)));
     HIPOK(hipMemset(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float)));
     HIPOK(hipMalloc((void**)&h->d_qctr, 4 * sizeof(unsigned)));
-    HIPOK(hipMalloc((void**)&h->d_stats, 8 * sizeof(unsigned long long)));
-    HIPOK(hipMemset(h->d_stats, 0, 8 * sizeof(unsigned long long)));
+    HIPOK(hipMalloc((void**)&h->d_stats, 16 * sizeof(unsigned long long)));
+    HIPOK(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
     for (auto& e : h->ev) HIPOK(hipEventCreate(&e));
 
     int occ = 0;
@@ -946,7 +1109,7 @@ void rtg_destroy(rtg_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_chunk(h);
-    (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodes4); (void)hipFree(h->d_tris); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
+    (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodesw); (void)hipFree(h->d_nodesq); (void)hipFree(h->d_leafbox); (void)hipFree(h->d_tris); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
     (void)hipFree(h->d_lights); (void)hipFree(h->d_texinfo); (void)hipFree(h->d_texels); (void)hipFree(h->d_film);
     (void)hipFree(h->d_pix); (void)hipFree(h->d_ovf); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
     for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
@@ -1158,7 +1321,7 @@ int rtg_clear(rtg_handle* h) {
     if (!h) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
     HIPOK(hipMemsetAsync(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float), h->stream));
-    HIPOK(hipMemsetAsync(h->d_stats, 0, 8 * sizeof(unsigned long long), h->stream));
+    HIPOK(hipMemsetAsync(h->d_stats, 0, 16 * sizeof(unsigned long long), h->stream));
     HIPOK(hipStreamSynchronize(h->stream));
     h->spp = 0;
     h->stats = rtg_stats{};
@@ -1169,7 +1332,7 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     if (!h || !out) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
     HIPOK(hipStreamSynchronize(h->stream));
-    unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long c[16] = {};
     HIPOK(hipMemcpy(c, h->d_stats, sizeof(c), hipMemcpyDeviceToHost));
     h->stats.node_visits = c[0];
     h->stats.tri_tests = c[1];
@@ -1177,6 +1340,9 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     h->stats.shadow_rays = c[3];
     h->stats.shadow_node_visits = c[4];
     h->stats.shadow_tri_tests = c[5];
+    h->stats.lane_slots = c[8];
+    h->stats.node_lane_steps = c[9];
+    h->stats.leaf_lane_steps = c[10];
     *out = h->stats;
     return RTG_OK;
 }
