@@ -12,9 +12,11 @@ def per_kernel(path, counter):
             acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     return acc
 
-def main(fetch_csv, write_csv, stats_csv, out_json):
+def main(fetch_csv, write_csv, stats_csv, out_json, dram_csv=None):
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
+    rq = per_kernel(dram_csv, "TCC_EA0_RDREQ_sum") if dram_csv else {}
+    rd = per_kernel(dram_csv, "TCC_EA0_RDREQ_DRAM_sum") if dram_csv else {}
     stats = {r["Name"]: r for r in csv.DictReader(open(stats_csv))}
     out = {"note": "per-launch averages; FETCH_SIZE/WRITE_SIZE in KiB from rocprofv3 --pmc (separate passes); "
                    "read bytes corrected x2 for gfx950 wide-stream under-count", "kernels": {}}
@@ -26,12 +28,18 @@ def main(fetch_csv, write_csv, stats_csv, out_json):
                              "read_bytes_corrected": round(fk * 1024 * 2), "write_bytes": round(wk * 1024),
                              "avg_ns_trace": float(st["AverageNs"]) if st else None,
                              "calls_trace": int(st["Calls"]) if st else None}
+        if k in rq and sum(rq[k]) > 0:
+            # share of L2 read requests that went to DRAM (the rest hit the Infinity Cache)
+            out["kernels"][k]["dram_share_of_l2_read_requests"] = round(sum(rd.get(k, [0])) / sum(rq[k]), 4)
     ext = [k for k in out["kernels"] if k.startswith("void k_trace<false, false>")]
     if ext:
         e = out["kernels"][ext[0]]
-        out["extend_hbm_bytes_per_launch"] = e["read_bytes_corrected"] + e["write_bytes"]
+        out["extend_l2_fabric_bytes_per_launch"] = e["read_bytes_corrected"] + e["write_bytes"]
+        share = e.get("dram_share_of_l2_read_requests")
+        out["extend_hbm_bytes_per_launch"] = (round(e["read_bytes_corrected"] * share) + e["write_bytes"]
+                                              if share is not None else e["read_bytes_corrected"] + e["write_bytes"])
     json.dump(out, open(out_json, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:6])
