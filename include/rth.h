@@ -56,6 +56,9 @@ int  rth_write_hdr(const char* path, int32_t width, int32_t height, const float*
 int  rth_read_hdr(const char* path, int32_t* width, int32_t* height, float** rgb);
 /* 8-bit PNG reader (stbi_load semantics). Caller frees with rth_free. */
 int  rth_read_png(const char* path, int32_t* width, int32_t* height, int32_t* channels, uint8_t** data);
+/* 8-bit texture decode as Texture::load's stbi_load sees it (Imaging.h:50): PNG or JPEG (baseline
+ * and progressive) chosen by content; channels = 1 or 3 for JPEG. Free with rth_free. */
+int  rth_read_ldr(const char* path, int32_t* width, int32_t* height, int32_t* channels, uint8_t** data);
 void rth_free(void* p);
 
 /* C3 synthetic scene: n_tris random triangles, splitmix64 stream from seed,

@@ -22,7 +22,7 @@ ORACLE_BUILD = os.path.join(ORACLE, "_build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RTG_ARCH", "gfx950")
 
-HOST_SRC = ["host/image_io.cpp", "host/gem_json.cpp", "host/scene_front.cpp"]
+HOST_SRC = ["host/image_io.cpp", "host/jpeg_decode.cpp", "host/gem_json.cpp", "host/scene_front.cpp"]
 DEVICE_SRC = ["device/rtg_kernels.hip"]
 
 
@@ -105,13 +105,14 @@ def build_ref(force=False):
 
 def stage_assets():
     """Copy reference scene data (not code) used by tests/bench into assets/ (git-ignored, travels
-    to the GPU box): coffee (config C5) and GI.hdr. Only when /root/reference is present."""
+    to the GPU box): coffee (config C5), bathroom (C4) and GI.hdr. Only when /root/reference is
+    present."""
     src = "/root/reference/RTBase"
     dst = os.path.join(ROOT, "assets")
     if not os.path.isdir(src):
         return
     os.makedirs(dst, exist_ok=True)
-    for name in ("coffee",):
+    for name in ("coffee", "bathroom"):
         if os.path.isdir(os.path.join(src, name)) and not os.path.isdir(os.path.join(dst, name)):
             shutil.copytree(os.path.join(src, name), os.path.join(dst, name))
     for f in ("GI.hdr",):

@@ -44,6 +44,16 @@ static int paeth(int a, int b, int c) {
     return c;
 }
 
+bool decode_ldr(const std::string& path, Image8& img, std::string& err) {
+    uint8_t head[8] = {};
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot read " + path; return false; }
+    size_t n = std::fread(head, 1, sizeof(head), f);
+    std::fclose(f);
+    if (n >= 2 && head[0] == 0xFF && head[1] == 0xD8) return decode_jpeg(path, img, err);
+    return decode_png(path, img, err);
+}
+
 // ---------------------------------------------------------------- PNG (non-interlaced)
 bool decode_png(const std::string& path, Image8& img, std::string& err) {
     std::vector<uint8_t> f;

@@ -18,6 +18,11 @@ struct ImageF {
 bool decode_png(const std::string& path, Image8& img, std::string& err);
 bool encode_png(const std::string& path, int w, int h, int channels, const uint8_t* rgb, std::string& err);
 bool decode_hdr(const std::string& path, ImageF& img, std::string& err);
+// JPEG (baseline + progressive, 8-bit; jpeg_decode.cpp)
+bool decode_jpeg(const std::string& path, Image8& img, std::string& err);
+bool decode_jpeg_mem(const uint8_t* data, size_t n, Image8& img, std::string& err);
+// PNG or JPEG by content (stbi_load's format sniffing for the formats RTBase scenes use)
+bool decode_ldr(const std::string& path, Image8& img, std::string& err);
 bool encode_hdr(const std::string& path, int w, int h, const float* rgb, std::string& err);
 
 }  // namespace rth

@@ -116,7 +116,7 @@ static TexData load_texture(const std::string& filename) {
         return t;
     }
     Image8 img;
-    if (!decode_png(filename, img, err) || img.width == 0 || img.height == 0) return t;
+    if (!decode_ldr(filename, img, err) || img.width == 0 || img.height == 0) return t;
     t.w = img.width;
     t.h = img.height;
     size_t n = (size_t)t.w * t.h;
@@ -516,6 +516,17 @@ int rth_read_hdr(const char* path, int32_t* w, int32_t* h, float** rgb) {
 int rth_read_png(const char* path, int32_t* w, int32_t* h, int32_t* ch, uint8_t** data) {
     Image8 img;
     if (!path || !decode_png(path, img, g_err)) return RTG_ERR_ARG;
+    *w = img.width;
+    *h = img.height;
+    *ch = img.channels;
+    *data = (uint8_t*)std::malloc(img.data.size());
+    std::memcpy(*data, img.data.data(), img.data.size());
+    return RTG_OK;
+}
+
+int rth_read_ldr(const char* path, int32_t* w, int32_t* h, int32_t* ch, uint8_t** data) {
+    Image8 img;
+    if (!path || !decode_ldr(path, img, g_err)) return RTG_ERR_ARG;
     *w = img.width;
     *h = img.height;
     *ch = img.channels;

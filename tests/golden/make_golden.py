@@ -106,7 +106,9 @@ def main():
     uv = rng.uniform(-3, 3, (2048, 2)).astype(np.float32)
     np.savez_compressed(os.path.join(GOLD, "env_tex_kat.npz"), dirs=dirs, env=rs.env_eval(rs.env_tex, dirs), uv=uv,
                         tex=rs.tex_sample(rs.env_tex, uv))
-    for fn in ("bathroom/floor_tiles.png", "bathroom/rug_mask.png", "GI.hdr", "materialball/envmap.hdr"):
+    for fn in ("bathroom/floor_tiles.png", "bathroom/rug_mask.png", "GI.hdr", "materialball/envmap.hdr",
+               "bathroom/marble.jpg", "bathroom/picture1.jpg", "bathroom/wallpaper-1.jpg",
+               "bathroom/wallpaper-2.jpg", "bathroom/wood.jpg", "bathroom/wood2.jpg"):
         p = os.path.join(REF, fn)
         if os.path.exists(p):
             t = pyref.load_texture(p)

@@ -194,6 +194,16 @@ def test_coffee_filtered_crop():
     assert_bitexact(gpu_film(s, 2), Oracle(s, 4, "rtm").render(2, seed=1234, threads=8)[0], "coffee_f")
 
 
+def test_bathroom_filtered_crop_depth16():
+    """Config C4's scene and depth (bathroom_f: JPEG/PNG textures, glass, mirror, Lambert stubs)."""
+    p = scene_path("bathroom")
+    if p is None:
+        pytest.skip("bathroom assets not staged on this machine")
+    s = loadScene(p, width=96, height=54, skip_missing=True)
+    assert_bitexact(gpu_film(s, 2, max_depth=16), Oracle(s, 16, "rtm").render(2, seed=1234, threads=8)[0],
+                    "bathroom_f depth 16")
+
+
 def test_scene_without_lights_is_rejected(tmp_path):
     src = os.path.relpath(os.path.join(SCENES, "cornell-box"), str(tmp_path))
     (tmp_path / "scene.json").write_text(
