@@ -7,6 +7,7 @@
  *   Texture::load                   RTBase/Imaging.h:32-71        (PNG / Radiance .hdr decode)
  *   Scene::init / Scene::build      RTBase/Scene.h:82-106,142-160 (BVH build, light list)
  *   Film::save                      RTBase/Imaging.h:262-271      -> rth_save_hdr()
+ *   Film::tonemap + savePNG         RTBase/Imaging.h:233-242, Renderer.h:895-898 -> rth_tonemap(), rth_save_png()
  *
  * It produces the flattened rtg_scene_desc consumed by rtg_create (include/rtg.h).
  */
@@ -50,6 +51,11 @@ int  rth_scene_permutation(const rth_scene* s, uint32_t* out /* n_tris */);
 
 /* Film::save: divide the accumulated sum by spp and write RLE RGBE (.hdr). */
 int  rth_save_hdr(const char* path, int32_t width, int32_t height, const float* rgb_sum, uint32_t spp);
+/* Film::tonemap (Imaging.h:233-242) for every pixel: (sum*exposure/(float)spp) clamped at 0,
+ * powf(.., 1/2.2f)*255 clamped at 255, truncated to a byte. rgb8 receives width*height*3 bytes. */
+int  rth_tonemap(int32_t width, int32_t height, const float* rgb_sum, uint32_t spp, float exposure, uint8_t* rgb8);
+/* RayTracer::savePNG (Renderer.h:895-898): tonemapped film written as an 8-bit RGB PNG. */
+int  rth_save_png(const char* path, int32_t width, int32_t height, const float* rgb_sum, uint32_t spp);
 /* Plain RGBE writer for an already-normalised float RGB image. */
 int  rth_write_hdr(const char* path, int32_t width, int32_t height, const float* rgb);
 /* Radiance .hdr reader (stbi_loadf semantics, 3 channels). Caller frees with rth_free. */

@@ -93,6 +93,8 @@ RTH_EXPORTS = [
     ("rth_read_hdr", C.c_int, [C.c_char_p, i32p, i32p, C.POINTER(f32p)]),
     ("rth_read_png", C.c_int, [C.c_char_p, i32p, i32p, i32p, C.POINTER(C.POINTER(C.c_uint8))]),
     ("rth_read_ldr", C.c_int, [C.c_char_p, i32p, i32p, i32p, C.POINTER(C.POINTER(C.c_uint8))]),
+    ("rth_tonemap", C.c_int, [C.c_int32, C.c_int32, f32p, C.c_uint32, C.c_float, C.POINTER(C.c_uint8)]),
+    ("rth_save_png", C.c_int, [C.c_char_p, C.c_int32, C.c_int32, f32p, C.c_uint32]),
     ("rth_free", None, [C.c_void_p]),
     ("rth_write_synthetic", C.c_int, [C.c_char_p, C.c_uint32, C.c_uint64, C.c_int32, C.c_int32]),
 ]

@@ -1,0 +1,96 @@
+// cli.cpp — headless counterpart of RTBase's Main.cpp (RTBase/Main.cpp:14-150) on librth + librtg.
+//
+// Same arguments and stopping rule as the reference's frame loop:
+//   -scene <dir>  -SPP <n>  -outputFilename <file>
+// frames of +1 spp until SPP is reached or 10 s of render time have passed, then the film is
+// written as result_<spp>.hdr (Film::save). The window / camera keys have no headless meaning;
+// 'P' and 'L' (saveHDR / savePNG of -outputFilename) become: -outputFilename is always written at
+// the end, as .hdr or, for a .png name, tonemapped PNG (RayTracer::savePNG).
+// Extra options (defaults keep the reference behaviour): -width -height (override scene.json),
+// -maxDepth (MAX_DEPTH, 4), -seed (sampler seed, 1234), -device, -batch (spp per rtg_render call;
+// results do not depend on it), -skipMissing 1 (filtered scene variants), -envmap <file>,
+// -timeLimit <s> (10; 0 = none).
+#include "../../../include/rth.h"
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+static int die(const char* what, const char* msg) {
+    std::fprintf(stderr, "rtg_render: %s: %s\n", what, msg ? msg : "");
+    return 1;
+}
+
+int main(int argc, char** argv) {
+    std::string scene_name = "MaterialsScene", filename = "GI.hdr";
+    unsigned spp_target = 8192;
+    std::unordered_map<std::string, std::string> args;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        if (!a.empty() && a[0] == '-') {
+            if (i + 1 < argc) args[a] = argv[++i];
+            else std::fprintf(stderr, "Error: Missing value for argument '%s'\n", a.c_str());
+        } else {
+            std::fprintf(stderr, "Warning: Ignoring unexpected argument '%s'\n", a.c_str());
+        }
+    }
+    auto get = [&](const char* k, const std::string& d) { auto it = args.find(k); return it == args.end() ? d : it->second; };
+    scene_name = get("-scene", scene_name);
+    filename = get("-outputFilename", filename);
+    spp_target = (unsigned)std::stoul(get("-SPP", std::to_string(spp_target)));
+    const bool out_given = args.count("-outputFilename") > 0;
+    rth_load_options lo{};
+    lo.width = std::stoi(get("-width", "0"));
+    lo.height = std::stoi(get("-height", "0"));
+    lo.skip_missing = std::stoi(get("-skipMissing", "0"));
+    std::string env = get("-envmap", "");
+    lo.envmap = env.empty() ? nullptr : env.c_str();
+    const int max_depth = std::stoi(get("-maxDepth", "4"));
+    const uint64_t seed = std::stoull(get("-seed", "1234"));
+    const int device = std::stoi(get("-device", "0"));
+    const unsigned batch = (unsigned)std::max(1, std::stoi(get("-batch", "1")));
+    const double time_limit = std::stod(get("-timeLimit", "10"));
+
+    rth_scene* scene = nullptr;
+    if (rth_load_scene(scene_name.c_str(), &lo, &scene) != 0) return die("loadScene", rth_last_error());
+    rth_scene_info info{};
+    rth_scene_get_info(scene, &info);
+    rtg_handle* rt = nullptr;
+    if (rtg_create(device, rth_scene_desc(scene), &rt) != 0) return die("rtg_create", rtg_last_error());
+    if (rtg_set_options(rt, max_depth, RTG_OPT_CULL, 0) != 0) return die("rtg_set_options", rtg_last_error());
+    std::printf("scene %s: %u triangles, %u lights, %dx%d (load %.0f ms, BVH %.0f ms)\n", scene_name.c_str(),
+                info.n_tris, info.n_lights, info.width, info.height, info.load_ms, info.bvh_ms);
+
+    unsigned spp = 0;
+    double total = 0.0;
+    while (spp < spp_target) {
+        const unsigned n = std::min(batch, spp_target - spp);
+        auto t0 = std::chrono::steady_clock::now();
+        if (rtg_render(rt, spp, n, seed, nullptr, 0) != 0) return die("rtg_render", rtg_last_error());
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        total += dt;
+        spp += n;
+        std::printf("Frame time: %gs | Total time: %gs\nSPP: %u\n", dt, total, spp);
+        if (time_limit > 0 && total >= time_limit) break;
+    }
+    std::vector<float> film((size_t)info.width * info.height * 3);
+    uint32_t got = 0;
+    if (rtg_film_read(rt, film.data(), &got) != 0) return die("rtg_film_read", rtg_last_error());
+    const std::string auto_name = "result_" + std::to_string(got) + ".hdr";
+    if (rth_save_hdr(auto_name.c_str(), info.width, info.height, film.data(), got) != 0)
+        return die("saveHDR", rth_last_error());
+    std::printf("wrote %s\n", auto_name.c_str());
+    if (out_given) {
+        const bool png = filename.size() > 4 && filename.compare(filename.size() - 4, 4, ".png") == 0;
+        int rc = png ? rth_save_png(filename.c_str(), info.width, info.height, film.data(), got)
+                     : rth_save_hdr(filename.c_str(), info.width, info.height, film.data(), got);
+        if (rc != 0) return die(png ? "savePNG" : "saveHDR", rth_last_error());
+        std::printf("wrote %s\n", filename.c_str());
+    }
+    rtg_destroy(rt);
+    rth_free_scene(scene);
+    return 0;
+}

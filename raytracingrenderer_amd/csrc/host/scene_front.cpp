@@ -524,6 +524,25 @@ int rth_read_png(const char* path, int32_t* w, int32_t* h, int32_t* ch, uint8_t*
     return RTG_OK;
 }
 
+int rth_tonemap(int32_t w, int32_t h, const float* sum, uint32_t spp, float exposure, uint8_t* out) {
+    if (!sum || !out || w <= 0 || h <= 0) { g_err = "rth_tonemap: bad argument"; return RTG_ERR_ARG; }
+    const size_t n = (size_t)w * h;
+    for (size_t i = 0; i < n * 3; ++i) {
+        const float p = sum[i] * exposure / (float)spp;
+        const float m = std::min(powf(std::max(p, 0.0f), 1.0f / 2.2f) * 255, 255.0f);
+        out[i] = (uint8_t)(m == m ? m : 0.0f);  // NaN (spp = 0 or a NaN film) -> 0
+    }
+    return RTG_OK;
+}
+
+int rth_save_png(const char* path, int32_t w, int32_t h, const float* sum, uint32_t spp) {
+    if (!path) { g_err = "rth_save_png: null path"; return RTG_ERR_ARG; }
+    std::vector<uint8_t> rgb((size_t)w * h * 3);
+    int rc = rth_tonemap(w, h, sum, spp, 1.0f, rgb.data());
+    if (rc) return rc;
+    return encode_png(path, w, h, 3, rgb.data(), g_err) ? RTG_OK : RTG_ERR_ARG;
+}
+
 int rth_read_ldr(const char* path, int32_t* w, int32_t* h, int32_t* ch, uint8_t** data) {
     Image8 img;
     if (!path || !decode_ldr(path, img, g_err)) return RTG_ERR_ARG;

@@ -122,6 +122,23 @@ def save_hdr(path, film_sum, spp):
     _check(N.rth().rth_save_hdr(os.fsencode(path), w, h, N.ptr(f, C.c_float), spp), N.rth().rth_last_error)
 
 
+def tonemap(film_sum, spp, exposure=1.0):
+    """Film::tonemap (Imaging.h:233-242) of every pixel -> uint8 RGB (H, W, 3)."""
+    f = np.ascontiguousarray(film_sum, np.float32)
+    h, w = f.shape[0], f.shape[1]
+    out = np.zeros((h, w, 3), np.uint8)
+    _check(N.rth().rth_tonemap(w, h, N.ptr(f, C.c_float), spp, exposure, N.ptr(out, C.c_uint8)),
+           N.rth().rth_last_error)
+    return out
+
+
+def save_png(path, film_sum, spp):
+    """RayTracer::savePNG (Renderer.h:895-898): tonemapped film as an 8-bit RGB PNG."""
+    f = np.ascontiguousarray(film_sum, np.float32)
+    h, w = f.shape[0], f.shape[1]
+    _check(N.rth().rth_save_png(os.fsencode(path), w, h, N.ptr(f, C.c_float), spp), N.rth().rth_last_error)
+
+
 def read_hdr(path):
     w, h = C.c_int32(), C.c_int32()
     p = N.f32p()
@@ -209,6 +226,10 @@ class RayTracer:
     def saveHDR(self, filename):
         f, spp = self.film()
         save_hdr(filename, f, max(spp, 1))
+
+    def savePNG(self, filename):
+        f, spp = self.film()
+        save_png(filename, f, spp)
 
     def stats(self):
         s = N.rtg_stats()
