@@ -25,24 +25,48 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+# BASELINE.json configs: scene, size, spp, MAX_DEPTH. C1 is the CPU-only case.
+CONFIGS = {
+    "C2": {"scene": "cornell-box", "width": 1024, "height": 1024, "spp": 64, "depth": 8},
+    "C3": {"scene": None, "width": 1024, "height": 1024, "spp": 64, "depth": 4},
+    "C4": {"scene": "bathroom", "width": 1920, "height": 1080, "spp": 256, "depth": 16, "skip_missing": True},
+    "C5": {"scene": "coffee", "width": 4096, "height": 4096, "spp": 1024, "depth": 4, "skip_missing": True,
+           "envmap": "GI.hdr"},
+}
+
+
+def scene_dir(name):
+    for base in (os.path.join(ROOT, "tests", "golden", "scenes"), os.path.join(ROOT, "assets"), "/root/reference/RTBase"):
+        p = os.path.join(base, name)
+        if os.path.isdir(p):
+            return p
+    raise SystemExit("scene %s not found (run __graft_entry__.build() where /root/reference exists)" % name)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--config", default="C3", choices=sorted(CONFIGS),
+                   help="BASELINE.json config; C3 is the headline metric, the others are side measurements")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--width", type=int, default=1024)
-    p.add_argument("--height", type=int, default=1024)
-    p.add_argument("--spp", type=int, default=64)
-    p.add_argument("--max-depth", type=int, default=4)
+    p.add_argument("--width", type=int, default=0, help="0 = the config's")
+    p.add_argument("--height", type=int, default=0, help="0 = the config's")
+    p.add_argument("--spp", type=int, default=0, help="0 = the config's")
+    p.add_argument("--max-depth", type=int, default=-1, help="-1 = the config's")
     p.add_argument("--tris", type=int, default=1_000_000)
     p.add_argument("--seed", type=int, default=20251015)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--bvh2", action="store_true", help="force the reference BVH2 walk (A/B)")
     p.add_argument("--max-paths", type=int, default=0, help="paths per wavefront chunk (0 = library default)")
-    return p.parse_args()
+    a = p.parse_args()
+    c = CONFIGS[a.config]
+    a.width = a.width or c["width"]
+    a.height = a.height or c["height"]
+    a.spp = a.spp or c["spp"]
+    a.max_depth = c["depth"] if a.max_depth < 0 else a.max_depth
+    return a
 
 
 def main():
@@ -61,10 +85,15 @@ def main():
     from raytracingrenderer_amd import _native as N
 
     # ---- scene (outside the timed region)
-    work = tempfile.mkdtemp(prefix="rtg_bench_r%d_" % rank)
+    cfg = CONFIGS[a.config]
     t0 = time.time()
-    write_synthetic_scene(work, n_tris=a.tris, seed=a.seed, width=a.width, height=a.height)
-    scene = loadScene(work)
+    if cfg["scene"] is None:
+        work = tempfile.mkdtemp(prefix="rtg_bench_r%d_" % rank)
+        write_synthetic_scene(work, n_tris=a.tris, seed=a.seed, width=a.width, height=a.height)
+        scene = loadScene(work)
+    else:
+        scene = loadScene(scene_dir(cfg["scene"]), width=a.width, height=a.height,
+                          skip_missing=cfg.get("skip_missing", False), envmap=cfg.get("envmap"))
     setup_s = time.time() - t0
     rt = RayTracer(scene, device=local, max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
     from raytracingrenderer_amd.distributed import reduce_film, tiles_for_rank
@@ -164,7 +193,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "Mray/s (closest-hit + shadow rays) at 1024x1024x64spp, synthetic 1M triangles",
+            "metric": ("Mray/s (closest-hit + shadow rays) at 1024x1024x64spp, synthetic 1M triangles"
+                       if a.config == "C3" else "Mray/s (closest-hit + shadow rays), config %s" % a.config),
             "value": round(mrays, 2),
             "unit": "Mray/s",
             "n_gpus": world,
@@ -178,9 +208,12 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (splitmix64 random triangles, generated in-run)",
-            "config": {"workload": "C3: synth-1M, %dx%d, %d spp, MAX_DEPTH %d" % (a.width, a.height, a.spp, a.max_depth),
-                       "triangles": a.tris, "width": a.width, "height": a.height, "spp": a.spp,
+            "data": ("synthetic (splitmix64 random triangles, generated in-run)" if cfg["scene"] is None
+                     else "reference scene assets (%s%s)" % (cfg["scene"], ", filtered" if cfg.get("skip_missing") else "")),
+            "config": {"workload": "%s: %s, %dx%d, %d spp, MAX_DEPTH %d" % (
+                           a.config, "synth-1M" if cfg["scene"] is None else cfg["scene"] + ("_f" if cfg.get("skip_missing") else ""),
+                           a.width, a.height, a.spp, a.max_depth),
+                       "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
                        "max_depth": a.max_depth, "parallelism": "tile-sharded x%d + RCCL film reduce" % world},
             "roofline": {"bound": "hbm", "kernel": "k_trace<closest>",
                          "achieved": None if achieved_gbs is None else round(achieved_gbs, 1),
@@ -192,6 +225,8 @@ def main():
                          "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from the reference BVH2)",
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
+                         "pops_per_ray": round(cw["pops"] / max(c_ext, 1), 2),
+                         "cullable_pops_per_ray": round(cw["cullable_pops"] / max(c_ext, 1), 2),
                          "lane_util_node_leaf": [round(cw["node_lane_steps"] / max(cw["lane_slots"], 1), 3),
                                                  round(cw["leaf_lane_steps"] / max(cw["lane_slots"], 1), 3)],
                          "avg_launch_ms": round(extend_ms / max(extend_launches, 1), 4)},
@@ -229,7 +264,7 @@ def cpu_baseline(scene, a):
             break
     dt = time.perf_counter() - t0
     return {"value": round(rays / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
-            "sample": "%d full %dx%d frame(s) at 1 spp of the same synth-1M scene (%d paths, %d rays) in %.1f s; "
+            "sample": "%d full %dx%d frame(s) at 1 spp of the same scene (%d paths, %d rays) in %.1f s; "
                       "oracle/rt_oracle.c tile renderer (reference DFS traversal, no culling), %d threads"
                       % (frames, scene.width, scene.height, paths, rays, dt, threads),
             "ms_per_frame": round(dt * 1e3 / frames, 1)}

@@ -115,9 +115,10 @@ def stage_assets():
     for name in ("coffee", "bathroom"):
         if os.path.isdir(os.path.join(src, name)) and not os.path.isdir(os.path.join(dst, name)):
             shutil.copytree(os.path.join(src, name), os.path.join(dst, name))
-    for f in ("GI.hdr",):
-        if os.path.exists(os.path.join(src, f)) and not os.path.exists(os.path.join(dst, f)):
-            shutil.copy(os.path.join(src, f), os.path.join(dst, f))
+    for f, into in (("GI.hdr", ""), ("GI.hdr", "coffee")):  # C5 = coffee_f + "envmap": "GI.hdr"
+        d = os.path.join(dst, into, f)
+        if os.path.exists(os.path.join(src, f)) and os.path.isdir(os.path.dirname(d)) and not os.path.exists(d):
+            shutil.copy(os.path.join(src, f), d)
 
 
 def build_all(force=False, device=True):

@@ -107,12 +107,13 @@ template <bool ANY, bool COUNT>
 __global__ __launch_bounds__(RTG_TB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
 void k_trace(SceneView s, TraceIO io) {
     __shared__ int stk[RTG_STACK][RTG_TB];
+    __shared__ float kstk[COUNT ? RTG_STACK : 1][RTG_TB];  // COUNT only: entry key of each push
     const int tid = threadIdx.x;
     const int lane = lane_id();
     const unsigned gthreads = gridDim.x * blockDim.x;
     const unsigned gtid = blockIdx.x * blockDim.x + tid;
     const unsigned n = *io.count;
-    unsigned long long c_nodes = 0, c_tris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0;
+    unsigned long long c_nodes = 0, c_tris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0, c_cullpop = 0, c_pops = 0;
     unsigned pool_base = 0, pool_left = 0;  // wave-uniform
     bool drained = false;                   // wave-uniform
     bool have = false;
@@ -167,8 +168,10 @@ void k_trace(SceneView s, TraceIO io) {
                     sp = 0;
                     // Wide walk only when every 1/d component is finite and nonzero (no NaN slab
                     // terms): then a passing descendant box implies its skipped ancestors pass.
-                    wide = io.wide && s.usew && fabsf(inv.x) <= RTG_FLT_MAX && fabsf(inv.y) <= RTG_FLT_MAX &&
-                            fabsf(inv.z) <= RTG_FLT_MAX && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
+                    // (|1/d| <= 2^64 and scene scale in [2^-60, 2^60] keep every product of the
+                    // compressed walk finite and normal.)
+                    wide = io.wide && s.usew && fabsf(inv.x) <= 0x1p64f && fabsf(inv.y) <= 0x1p64f &&
+                           fabsf(inv.z) <= 0x1p64f && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
                     const float* rb = s.root_box;
                     cur = slab_exact(rb[0], rb[1], rb[2], rb[3], rb[4], rb[5], o, inv)
                               ? (wide ? s.root_wordw : s.root_word) : RTG_EXIT;
@@ -186,9 +189,9 @@ void k_trace(SceneView s, TraceIO io) {
         if (!have || cur == RTG_EXIT) continue;
         // ---- one traversal step
         if (cur >= 0 && wide) {
-            float pl[6][RTG_WIDTH];
             int wd[RTG_WIDTH];
             float key[RTG_WIDTH];
+            int nh = 0;
 #if RTG_QNODE
             {
                 const float4* np = s.nodesq[cur].q;
@@ -199,21 +202,53 @@ void k_trace(SceneView s, TraceIO io) {
                 const float sz = __uint_as_float(((ex >> 16) & 255u) << 23);
                 const unsigned p0 = __float_as_uint(h1.x), p1 = __float_as_uint(h1.y), p2 = __float_as_uint(h1.z);
                 const unsigned p3 = __float_as_uint(h1.w), p4 = __float_as_uint(h2.x), p5 = __float_as_uint(h2.y);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    pl[0][k] = qdecode(h0.x, p0, k, sx);
-                    pl[1][k] = qdecode(h0.y, p1, k, sy);
-                    pl[2][k] = qdecode(h0.z, p2, k, sz);
-                    pl[3][k] = qdecode(h0.x, p3, k, sx);
-                    pl[4][k] = qdecode(h0.y, p4, k, sy);
-                    pl[5][k] = qdecode(h0.z, p5, k, sz);
-                }
                 wd[0] = __float_as_int(h2.z);
                 wd[1] = __float_as_int(h2.w);
                 wd[2] = __float_as_int(h3.x);
                 wd[3] = __float_as_int(h3.y);
+                // Conservative slot test in ray-relative form. Exactness does not need the exact slab
+                // test here: a candidate hit is accepted only after its reference leaf box passes the
+                // exact test, so a slot test only has to pass whenever the exact test on a reference
+                // box inside the slot passes. Per axis, with s the power-of-two step:
+                //   near entry  tn = fma(q_near, s*inv, ((origin + mn) - o) * inv)
+                //   far exit    tf = fma(q_far,  s*inv, ((origin - mn) - o) * inv)
+                // mn moves the near plane (and -mn the far plane) outward by mu = 2^-16 (scale + |o|).
+                // The rounding of this form plus the reference's own is below 2^-19.5 (scale + |o|)|inv|
+                // per plane, inside the mu |inv| margin, so tn <= the reference entry
+                // and tf >= the reference exit of every box the slot contains.
+                // Cull key: max(tn) - (delta - mu) * max|inv| is below the entry of the slot's box
+                // inflated by delta (slab_cull_entry's conservative bound).
+                const bool px = inv.x > 0.0f, py = inv.y > 0.0f, pz = inv.z > 0.0f;
+                const unsigned nqx = px ? p0 : p3, fqx = px ? p3 : p0;
+                const unsigned nqy = py ? p1 : p4, fqy = py ? p4 : p1;
+                const unsigned nqz = pz ? p2 : p5, fqz = pz ? p5 : p2;
+                const float mu = RTG_CULL_REL * omag;
+                const float mnx = px ? -mu : mu, mny = py ? -mu : mu, mnz = pz ? -mu : mu;
+                const float anx = ((h0.x + mnx) - o.x) * inv.x, afx = ((h0.x - mnx) - o.x) * inv.x;
+                const float any_ = ((h0.y + mny) - o.y) * inv.y, afy = ((h0.y - mny) - o.y) * inv.y;
+                const float anz = ((h0.z + mnz) - o.z) * inv.z, afz = ((h0.z - mnz) - o.z) * inv.z;
+                const float six = sx * inv.x, siy = sy * inv.y, siz = sz * inv.z;
+                const float cshift = (delta - mu) * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z));
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float tnx = fmaf((float)((nqx >> (8 * k)) & 255u), six, anx);
+                    const float tny = fmaf((float)((nqy >> (8 * k)) & 255u), siy, any_);
+                    const float tnz = fmaf((float)((nqz >> (8 * k)) & 255u), siz, anz);
+                    const float tfx = fmaf((float)((fqx >> (8 * k)) & 255u), six, afx);
+                    const float tfy = fmaf((float)((fqy >> (8 * k)) & 255u), siy, afy);
+                    const float tfz = fmaf((float)((fqz >> (8 * k)) & 255u), siz, afz);
+                    const float en = fmaxf(fmaxf(tnx, tny), tnz);
+                    const float tx = fminf(fminf(tfx, tfy), tfz);
+                    const float e = en - cshift;
+                    bool hit = wd[k] != RTG_EXIT && !(tx < en || tx < 0.0f);
+                    if (io.cull) hit = hit && !(e > tbest);
+                    if (COUNT) c_nodes += wd[k] != RTG_EXIT ? 1 : 0;
+                    key[k] = hit ? fmaxf(e, -RTG_FLT_MAX) : __builtin_inff();
+                    nh += hit ? 1 : 0;
+                }
             }
 #else
+            float pl[6][RTG_WIDTH];
             const float4* np = s.nodesw[cur].q;
 #pragma unroll
             for (int q = 0; q < 6 * RTG_WQ; ++q) {
@@ -231,8 +266,6 @@ void k_trace(SceneView s, TraceIO io) {
                 wd[q * 4 + 2] = __float_as_int(v.z);
                 wd[q * 4 + 3] = __float_as_int(v.w);
             }
-#endif
-            int nh = 0;
 #pragma unroll
             for (int k = 0; k < RTG_WIDTH; ++k) {
                 const float mnx = pl[0][k], mny = pl[1][k], mnz = pl[2][k];
@@ -244,6 +277,7 @@ void k_trace(SceneView s, TraceIO io) {
                 key[k] = hit ? fmaxf(e, -RTG_FLT_MAX) : __builtin_inff();
                 nh += hit ? 1 : 0;
             }
+#endif
             // ascending entry distance (misses sort last); order only affects culling, not results
 #define RTG_CSWAP(i, j)                                               \
     if (key[j] < key[i]) {                                           \
@@ -267,6 +301,7 @@ void k_trace(SceneView s, TraceIO io) {
 #pragma unroll
                 for (int k = RTG_WIDTH - 1; k >= 1; --k) {
                     if (k < nh) {
+                        if (COUNT && sp < RTG_STACK) kstk[sp][tid] = key[k];
                         if (sp < RTG_STACK) stk[sp][tid] = wd[k];
                         else io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid] = wd[k];
                         ++sp;
@@ -289,6 +324,7 @@ void k_trace(SceneView s, TraceIO io) {
                 const bool lfirst = !(er < el);
                 const int nearw = lfirst ? nd.d.x : nd.d.y;
                 const int farw = lfirst ? nd.d.y : nd.d.x;
+                if (COUNT && sp < RTG_STACK) kstk[sp][tid] = -RTG_FLT_MAX;
                 if (sp < RTG_STACK) stk[sp][tid] = farw;
                 else io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid] = farw;
                 ++sp;
@@ -340,11 +376,13 @@ void k_trace(SceneView s, TraceIO io) {
         // ---- one pop for every branch: always an LDS read (ds_read, not a flat load through a
         // selected pointer); the global overflow read only for deep entries
         if (cur == RTG_POP) {
+            if (COUNT && !ANY && sp > 0) c_pops += 1;
             if (sp == 0) {
                 cur = RTG_EXIT;
             } else {
                 --sp;
                 cur = stk[sp < RTG_STACK ? sp : 0][tid];
+                if (COUNT && !ANY && sp < RTG_STACK && kstk[sp][tid] > tbest) c_cullpop += 1;
                 if (sp >= RTG_STACK) cur = io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
             }
         }
@@ -355,6 +393,8 @@ void k_trace(SceneView s, TraceIO io) {
             c_tris += __shfl_down(c_tris, off);
             c_nstep += __shfl_down(c_nstep, off);
             c_lstep += __shfl_down(c_lstep, off);
+            c_cullpop += __shfl_down(c_cullpop, off);
+            c_pops += __shfl_down(c_pops, off);
         }
         if (lane == 0) {
             atomicAdd(&io.stats[ANY ? 4 : 0], c_nodes);
@@ -363,6 +403,8 @@ void k_trace(SceneView s, TraceIO io) {
                 atomicAdd(&io.stats[8], c_slots);
                 atomicAdd(&io.stats[9], c_nstep);
                 atomicAdd(&io.stats[10], c_lstep);
+                atomicAdd(&io.stats[11], c_cullpop);
+                atomicAdd(&io.stats[12], c_pops);
             }
         }
     }
@@ -968,7 +1010,11 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             std::memcpy(&nodesw[nw], f, sizeof(DevNodeW));
         }
     }
-    h->usew = finite && qok && nt > 0;
+    float cull_scale = 0.0f;
+    for (int k = 0; k < 6; ++k)
+        if (std::isfinite(d->node_bounds[k])) cull_scale = std::max(cull_scale, std::fabs(d->node_bounds[k]));
+    // the compressed walk's rounding margin is stated relative to the scene scale (k_trace)
+    h->usew = finite && qok && nt > 0 && (!RTG_QNODE || (cull_scale >= 0x1p-60f && cull_scale <= 0x1p60f));
     // exact leaf boxes per triangle (compressed walk: candidate hits re-test their leaf)
     std::vector<float4> leafbox(RTG_QNODE ? std::max<size_t>((size_t)nt * 2, 2) : 2);
     if (RTG_QNODE) {
@@ -1343,6 +1389,8 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     h->stats.lane_slots = c[8];
     h->stats.node_lane_steps = c[9];
     h->stats.leaf_lane_steps = c[10];
+    h->stats.cullable_pops = c[11];
+    h->stats.pops = c[12];
     *out = h->stats;
     return RTG_OK;
 }

@@ -80,6 +80,32 @@ def test_wide_walk_is_exact(cornell256, synth20k):
         assert np.array_equal(a.trace_visible(r), b.trace_visible(r))
 
 
+def test_wide_walk_adversarial_rays(synth20k, cornell256):
+    """Rays that start on reference box faces/corners and run (nearly) along box planes: the
+    compressed walk's conservative slot test must never lose a reachable leaf."""
+    rng = np.random.default_rng(21)
+    for s in (synth20k, cornell256):
+        nb = s.node_bounds
+        n = 60000
+        pick = rng.integers(0, len(nb), n)
+        corner = rng.integers(0, 2, (n, 3))
+        o = np.where(corner == 0, nb[pick, 0:3], nb[pick, 3:6]).astype(np.float32)
+        axis = np.eye(3, dtype=np.float32)[rng.integers(0, 3, n)] * rng.choice([-1, 1], (n, 1)).astype(np.float32)
+        eps = np.float32(10.0) ** rng.uniform(-7, -1, (n, 1)).astype(np.float32)
+        d = axis + eps * rng.normal(size=(n, 3)).astype(np.float32)
+        d[: n // 6] = rng.normal(size=(n // 6, 3))  # plus generic directions from box corners
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        r = np.zeros((n, 8), np.float32)
+        r[:, :3] = o
+        r[:, 4:7] = d
+        r[:, 3] = rng.uniform(0.01, 4, n)
+        for cull in (True, False):
+            a = RayTracer(s, cull=cull, wide=True)
+            b = RayTracer(s, cull=cull, wide=False)
+            assert_bitexact(a.trace_closest(r), b.trace_closest(r), "adversarial closest")
+            assert np.array_equal(a.trace_visible(r), b.trace_visible(r))
+
+
 @pytest.mark.parametrize("max_depth", [0, 1, 8, 16])
 def test_depths_cornell_materials(max_depth):
     """glass / mirror / Lambert stubs (one- and two-sided) / env + area lights (configs C2, C4 depth)."""
