@@ -40,6 +40,9 @@ using namespace rtgd;
 #ifndef RTG_STACK
 #define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (24 KB per block)
 #endif
+#ifndef RTG_POSTPONE
+#define RTG_POSTPONE 32     // >0: park a reached leaf and keep walking; run the leaves of a wave together
+#endif                      //     once this many lanes hold one (or no lane can walk on)
 #ifndef RTG_TRACE_WPE
 #define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel
 #endif
@@ -120,11 +123,11 @@ void k_trace(SceneView s, TraceIO io) {
     unsigned ri = 0;
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tbest = 0.0f, omag = 0.0f, dmag = 0.0f, delta = 0.0f, bu = 0.0f, bv = 0.0f;
-    int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0;
+    int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0, pend = RTG_EXIT;
     bool occluded = false, wide = false;
     for (;;) {
         // ---- retire finished rays
-        if (have && cur == RTG_EXIT) {
+        if (have && cur == RTG_EXIT && pend == RTG_EXIT) {
             if (ANY) {
                 if (io.visible) io.visible[pid] = occluded ? 0 : 1;
                 else if (!occluded) io.contrib[pid] = io.ray_c[pid];
@@ -166,6 +169,7 @@ void k_trace(SceneView s, TraceIO io) {
                     bu = bv = 0.0f;
                     occluded = false;
                     sp = 0;
+                    pend = RTG_EXIT;
                     // Wide walk only when every 1/d component is finite and nonzero (no NaN slab
                     // terms): then a passing descendant box implies its skipped ancestors pass.
                     // (|1/d| <= 2^64 and scene scale in [2^-60, 2^60] keep every product of the
@@ -186,7 +190,44 @@ void k_trace(SceneView s, TraceIO io) {
             c_nstep += (have && cur >= 0) ? 1 : 0;
             c_lstep += (have && cur != RTG_EXIT && cur < 0) ? 1 : 0;
         }
-        if (!have || cur == RTG_EXIT) continue;
+        if (!have || (cur == RTG_EXIT && pend == RTG_EXIT)) continue;
+        // Leaf: the reference's leaf loop (Geometry.h:420-431 / 446-458) over 1-2 triangles.
+        auto leaf = [&](const int word) {
+            const int code = ~word;
+            const int start = code >> 1;
+            const int cnt = (code & 1) + 1;
+            bool lchk = false, lok = true;  // exact leaf box, tested on the first candidate only
+            for (int k = 0; k < cnt; ++k) {
+                const int tri = start + k;
+                if (COUNT) c_tris += 1;
+                const DevTri T = s.tris[tri];
+                float t, u, v;
+                if (tri_intersect(T, o, d, t, u, v)) {
+                    bool cand = ANY ? !(t >= tbest || t <= RTG_EPS)
+                                    : (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid)));
+#if RTG_QNODE
+                    if (cand && wide) {
+                        if (!lchk) {
+                            const float4 b0 = s.leafbox[2 * start], b1 = s.leafbox[2 * start + 1];
+                            lok = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
+                            lchk = true;
+                        }
+                        cand = lok;
+                    }
+#endif
+                    if (!cand) {
+                    } else if (ANY) {
+                        occluded = true;
+                    } else {
+                        tbest = t;
+                        bid = tri;
+                        bu = u;
+                        bv = v;
+                        delta = RTG_CULL_REL * (omag + tbest * dmag);
+                    }
+                }
+            }
+        };
         // ---- one traversal step
         if (cur >= 0 && wide) {
             int wd[RTG_WIDTH];
@@ -336,43 +377,19 @@ void k_trace(SceneView s, TraceIO io) {
             } else {
                 cur = RTG_POP;
             }
-        } else {
-            const int code = ~cur;
-            const int start = code >> 1;
-            const int cnt = (code & 1) + 1;
-            bool lchk = false, lok = true;  // exact leaf box, tested on the first candidate only
-            for (int k = 0; k < cnt; ++k) {
-                const int tri = start + k;
-                if (COUNT) c_tris += 1;
-                const DevTri T = s.tris[tri];
-                float t, u, v;
-                if (tri_intersect(T, o, d, t, u, v)) {
-                    bool cand = ANY ? !(t >= tbest || t <= RTG_EPS)
-                                    : (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid)));
-#if RTG_QNODE
-                    if (cand && wide) {
-                        if (!lchk) {
-                            const float4 b0 = s.leafbox[2 * start], b1 = s.leafbox[2 * start + 1];
-                            lok = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
-                            lchk = true;
-                        }
-                        cand = lok;
-                    }
-#endif
-                    if (!cand) {
-                    } else if (ANY) {
-                        occluded = true;
-                    } else {
-                        tbest = t;
-                        bid = tri;
-                        bu = u;
-                        bv = v;
-                        delta = RTG_CULL_REL * (omag + tbest * dmag);
-                    }
-                }
-            }
+        }
+#if RTG_POSTPONE
+        // park a reached leaf (one per lane) and keep walking
+        if (cur < 0 && cur != RTG_EXIT && cur != RTG_POP && pend == RTG_EXIT) {
+            pend = cur;
+            cur = RTG_POP;
+        }
+#else
+        else if (cur != RTG_EXIT) {
+            leaf(cur);
             cur = (ANY && occluded) ? RTG_EXIT : RTG_POP;
         }
+#endif
         // ---- one pop for every branch: always an LDS read (ds_read, not a flat load through a
         // selected pointer); the global overflow read only for deep entries
         if (cur == RTG_POP) {
@@ -386,6 +403,20 @@ void k_trace(SceneView s, TraceIO io) {
                 if (sp >= RTG_STACK) cur = io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
             }
         }
+#if RTG_POSTPONE
+        // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on
+        const unsigned long long pm = __ballot(pend != RTG_EXIT);
+        if (__popcll(pm) >= RTG_POSTPONE || __ballot(cur >= 0) == 0) {
+            if (pend != RTG_EXIT) {
+                leaf(pend);
+                pend = RTG_EXIT;
+                if (ANY && occluded) {
+                    cur = RTG_EXIT;
+                    sp = 0;
+                }
+            }
+        }
+#endif
     }
     if (COUNT) {
         for (int off = 32; off > 0; off >>= 1) {
