@@ -227,8 +227,11 @@ def main():
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
                          "pops_per_ray": round(cw["pops"] / max(c_ext, 1), 2),
                          "cullable_pops_per_ray": round(cw["cullable_pops"] / max(c_ext, 1), 2),
+                         # node: lanes stepping a node per loop iteration; leaf: lanes running a
+                         # parked leaf per leaf phase; leaf phases per iteration
                          "lane_util_node_leaf": [round(cw["node_lane_steps"] / max(cw["lane_slots"], 1), 3),
-                                                 round(cw["leaf_lane_steps"] / max(cw["lane_slots"], 1), 3)],
+                                                 round(cw["leaf_lane_steps"] / max(cw["leaf_phase_slots"], 1), 3),
+                                                 round(cw["leaf_phase_slots"] / max(cw["lane_slots"], 1), 3)],
                          "avg_launch_ms": round(extend_ms / max(extend_launches, 1), 4)},
             "kernel_ms_per_step_rank0": {"closest_hit": round(local_kernel_ms[0] / a.steps, 2),
                                          "any_hit": round(local_kernel_ms[1] / a.steps, 2),

@@ -103,6 +103,7 @@ typedef struct rtg_stats {
     uint64_t lane_slots;           /* RTG_OPT_COUNT: closest-hit loop iterations x 64 lanes     */
     uint64_t node_lane_steps;      /* RTG_OPT_COUNT: lanes doing a node step, summed            */
     uint64_t leaf_lane_steps;      /* RTG_OPT_COUNT: lanes doing a leaf step, summed            */
+    uint64_t leaf_phase_slots;     /* RTG_OPT_COUNT: leaf-phase iterations x 64 lanes           */
     uint64_t pops;                 /* RTG_OPT_COUNT: closest-hit stack pops                     */
     uint64_t cullable_pops;        /* RTG_OPT_COUNT: pops whose entry distance was > the hit    */
 } rtg_stats;

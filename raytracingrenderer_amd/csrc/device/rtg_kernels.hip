@@ -43,6 +43,9 @@ using namespace rtgd;
 #ifndef RTG_POSTPONE
 #define RTG_POSTPONE 32     // >0: park a reached leaf and keep walking; run the leaves of a wave together
 #endif                      //     once this many lanes hold one (or no lane can walk on)
+#ifndef RTG_REFILL
+#define RTG_REFILL 1        // refill idle lanes once at least this many are idle (the setup code then
+#endif                      // runs with more lanes per execution)
 #ifndef RTG_TRACE_WPE
 #define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel
 #endif
@@ -116,7 +119,7 @@ void k_trace(SceneView s, TraceIO io) {
     const unsigned gthreads = gridDim.x * blockDim.x;
     const unsigned gtid = blockIdx.x * blockDim.x + tid;
     const unsigned n = *io.count;
-    unsigned long long c_nodes = 0, c_tris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0, c_cullpop = 0, c_pops = 0;
+    unsigned long long c_nodes = 0, c_tris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0, c_cullpop = 0, c_pops = 0, c_lslots = 0;
     unsigned pool_base = 0, pool_left = 0;  // wave-uniform
     bool drained = false;                   // wave-uniform
     bool have = false;
@@ -138,7 +141,7 @@ void k_trace(SceneView s, TraceIO io) {
         }
         // ---- refill idle lanes from the wave's pool
         const unsigned long long im = __ballot(!have);
-        if (im != 0 && !drained) {
+        if (im != 0 && !drained && (__popcll(im) >= RTG_REFILL || __ballot(have) == 0)) {
             if (pool_left == 0) {
                 unsigned b = 0;
                 if (lane == 0) b = atomicAdd(io.fetch, 64u);
@@ -188,7 +191,7 @@ void k_trace(SceneView s, TraceIO io) {
         if (COUNT && !ANY) {
             c_slots += 64;
             c_nstep += (have && cur >= 0) ? 1 : 0;
-            c_lstep += (have && cur != RTG_EXIT && cur < 0) ? 1 : 0;
+            if (!RTG_POSTPONE) c_lstep += (have && cur != RTG_EXIT && cur < 0) ? 1 : 0;
         }
         if (!have || (cur == RTG_EXIT && pend == RTG_EXIT)) continue;
         // Leaf: the reference's leaf loop (Geometry.h:420-431 / 446-458) over 1-2 triangles.
@@ -232,7 +235,6 @@ void k_trace(SceneView s, TraceIO io) {
         if (cur >= 0 && wide) {
             int wd[RTG_WIDTH];
             float key[RTG_WIDTH];
-            int nh = 0;
 #if RTG_QNODE
             {
                 const float4* np = s.nodesq[cur].q;
@@ -281,11 +283,10 @@ void k_trace(SceneView s, TraceIO io) {
                     const float en = fmaxf(fmaxf(tnx, tny), tnz);
                     const float tx = fminf(fminf(tfx, tfy), tfz);
                     const float e = en - cshift;
-                    bool hit = wd[k] != RTG_EXIT && !(tx < en || tx < 0.0f);
-                    if (io.cull) hit = hit && !(e > tbest);
+                    // (finite here, so a miss is the only +inf key)
+                    const bool hit = wd[k] != RTG_EXIT && !(tx < en || tx < 0.0f) && (!io.cull || !(e > tbest));
                     if (COUNT) c_nodes += wd[k] != RTG_EXIT ? 1 : 0;
-                    key[k] = hit ? fmaxf(e, -RTG_FLT_MAX) : __builtin_inff();
-                    nh += hit ? 1 : 0;
+                    key[k] = hit ? e : __builtin_inff();
                 }
             }
 #else
@@ -316,7 +317,6 @@ void k_trace(SceneView s, TraceIO io) {
                 if (io.cull) hit = hit && !(e > tbest);
                 if (COUNT) c_nodes += wd[k] != RTG_EXIT ? 1 : 0;
                 key[k] = hit ? fmaxf(e, -RTG_FLT_MAX) : __builtin_inff();
-                nh += hit ? 1 : 0;
             }
 #endif
             // ascending entry distance (misses sort last); order only affects culling, not results
@@ -336,12 +336,13 @@ void k_trace(SceneView s, TraceIO io) {
             RTG_CSWAP(1, 2) RTG_CSWAP(3, 4) RTG_CSWAP(5, 6)
 #endif
 #undef RTG_CSWAP
-            if (nh == 0) {
+            // misses carry +inf and sort last
+            if (key[0] == __builtin_inff()) {
                 cur = RTG_POP;
             } else {
 #pragma unroll
                 for (int k = RTG_WIDTH - 1; k >= 1; --k) {
-                    if (k < nh) {
+                    if (key[k] != __builtin_inff()) {
                         if (COUNT && sp < RTG_STACK) kstk[sp][tid] = key[k];
                         if (sp < RTG_STACK) stk[sp][tid] = wd[k];
                         else io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid] = wd[k];
@@ -407,6 +408,10 @@ void k_trace(SceneView s, TraceIO io) {
         // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on
         const unsigned long long pm = __ballot(pend != RTG_EXIT);
         if (__popcll(pm) >= RTG_POSTPONE || __ballot(cur >= 0) == 0) {
+            if (COUNT && !ANY) {
+                c_lslots += 64;
+                c_lstep += pend != RTG_EXIT ? 1 : 0;
+            }
             if (pend != RTG_EXIT) {
                 leaf(pend);
                 pend = RTG_EXIT;
@@ -434,6 +439,7 @@ void k_trace(SceneView s, TraceIO io) {
                 atomicAdd(&io.stats[8], c_slots);
                 atomicAdd(&io.stats[9], c_nstep);
                 atomicAdd(&io.stats[10], c_lstep);
+                atomicAdd(&io.stats[13], c_lslots);
                 atomicAdd(&io.stats[11], c_cullpop);
                 atomicAdd(&io.stats[12], c_pops);
             }
@@ -1420,6 +1426,7 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     h->stats.lane_slots = c[8];
     h->stats.node_lane_steps = c[9];
     h->stats.leaf_lane_steps = c[10];
+    h->stats.leaf_phase_slots = c[13];
     h->stats.cullable_pops = c[11];
     h->stats.pops = c[12];
     *out = h->stats;
