@@ -44,7 +44,7 @@ using namespace rtgd;
 #define RTG_POSTPONE 32     // >0: park a reached leaf and keep walking; run the leaves of a wave together
 #endif                      //     once this many lanes hold one (or no lane can walk on)
 #ifndef RTG_REFILL
-#define RTG_REFILL 1        // refill idle lanes once at least this many are idle (the setup code then
+#define RTG_REFILL 16       // refill idle lanes once at least this many are idle (the setup code then
 #endif                      // runs with more lanes per execution)
 #ifndef RTG_TRACE_WPE
 #define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel
