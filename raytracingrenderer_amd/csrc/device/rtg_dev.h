@@ -109,6 +109,7 @@ struct __align__(16) DevNodeW {
 struct __align__(16) DevNodeQ {
     float4 q[4];
 };
+typedef float f2 __attribute__((ext_vector_type(2)));  // packed FP32 pair (v_pk_fma/mul/add_f32)
 __host__ __device__ inline float qdecode(float origin, unsigned plane, int k, float scale) {
     return origin + (float)((plane >> (8 * k)) & 255u) * scale;
 }

@@ -267,26 +267,38 @@ void k_trace(SceneView s, TraceIO io) {
                 const unsigned nqz = pz ? p2 : p5, fqz = pz ? p5 : p2;
                 const float mu = RTG_CULL_REL * omag;
                 const float mnx = px ? -mu : mu, mny = py ? -mu : mu, mnz = pz ? -mu : mu;
-                const float anx = ((h0.x + mnx) - o.x) * inv.x, afx = ((h0.x - mnx) - o.x) * inv.x;
-                const float any_ = ((h0.y + mny) - o.y) * inv.y, afy = ((h0.y - mny) - o.y) * inv.y;
-                const float anz = ((h0.z + mnz) - o.z) * inv.z, afz = ((h0.z - mnz) - o.z) * inv.z;
+                // packed FP32 (v_pk_*): per-component IEEE results identical to the scalar ops
+                const f2 ax2 = ((f2){h0.x, h0.x} + (f2){mnx, -mnx} - (f2){o.x, o.x}) * (f2){inv.x, inv.x};
+                const f2 ay2 = ((f2){h0.y, h0.y} + (f2){mny, -mny} - (f2){o.y, o.y}) * (f2){inv.y, inv.y};
+                const f2 az2 = ((f2){h0.z, h0.z} + (f2){mnz, -mnz} - (f2){o.z, o.z}) * (f2){inv.z, inv.z};
                 const float six = sx * inv.x, siy = sy * inv.y, siz = sz * inv.z;
+                const f2 six2 = {six, six}, siy2 = {siy, siy}, siz2 = {siz, siz};
+                const f2 anx2 = {ax2.x, ax2.x}, afx2 = {ax2.y, ax2.y};
+                const f2 any2 = {ay2.x, ay2.x}, afy2 = {ay2.y, ay2.y};
+                const f2 anz2 = {az2.x, az2.x}, afz2 = {az2.y, az2.y};
                 const float cshift = (delta - mu) * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z));
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float tnx = fmaf((float)((nqx >> (8 * k)) & 255u), six, anx);
-                    const float tny = fmaf((float)((nqy >> (8 * k)) & 255u), siy, any_);
-                    const float tnz = fmaf((float)((nqz >> (8 * k)) & 255u), siz, anz);
-                    const float tfx = fmaf((float)((fqx >> (8 * k)) & 255u), six, afx);
-                    const float tfy = fmaf((float)((fqy >> (8 * k)) & 255u), siy, afy);
-                    const float tfz = fmaf((float)((fqz >> (8 * k)) & 255u), siz, afz);
-                    const float en = fmaxf(fmaxf(tnx, tny), tnz);
-                    const float tx = fminf(fminf(tfx, tfy), tfz);
-                    const float e = en - cshift;
-                    // (finite here, so a miss is the only +inf key)
-                    const bool hit = wd[k] != RTG_EXIT && !(tx < en || tx < 0.0f) && (!io.cull || !(e > tbest));
-                    if (COUNT) c_nodes += wd[k] != RTG_EXIT ? 1 : 0;
-                    key[k] = hit ? e : __builtin_inff();
+                for (int k = 0; k < 4; k += 2) {  // slot pairs (k, k+1)
+                    auto q2 = [&](unsigned plane) {
+                        return (f2){(float)((plane >> (8 * k)) & 255u), (float)((plane >> (8 * k + 8)) & 255u)};
+                    };
+                    const f2 tnx = __builtin_elementwise_fma(q2(nqx), six2, anx2);
+                    const f2 tny = __builtin_elementwise_fma(q2(nqy), siy2, any2);
+                    const f2 tnz = __builtin_elementwise_fma(q2(nqz), siz2, anz2);
+                    const f2 tfx = __builtin_elementwise_fma(q2(fqx), six2, afx2);
+                    const f2 tfy = __builtin_elementwise_fma(q2(fqy), siy2, afy2);
+                    const f2 tfz = __builtin_elementwise_fma(q2(fqz), siz2, afz2);
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const float en = fmaxf(fmaxf(tnx[j], tny[j]), tnz[j]);
+                        const float tx = fminf(fminf(tfx[j], tfy[j]), tfz[j]);
+                        const float e = en - cshift;
+                        // (finite here, so a miss is the only +inf key)
+                        // (bitwise & / |: no branches per slot)
+                        const bool hit = (wd[k + j] != RTG_EXIT) & !((tx < en) | (tx < 0.0f)) & (!io.cull | !(e > tbest));
+                        if (COUNT) c_nodes += wd[k + j] != RTG_EXIT ? 1 : 0;
+                        key[k + j] = hit ? e : __builtin_inff();
+                    }
                 }
             }
 #else
