@@ -59,6 +59,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--bvh2", action="store_true", help="force the reference BVH2 walk (A/B)")
+    p.add_argument("--shard-of", type=int, default=0,
+                   help="diagnostic: render only rank 0's tiles of this many ranks, on one GPU, to see the "
+                        "per-GPU rate at that world size (value is then this GPU's rate, not a job total)")
+    p.add_argument("--verify-film", action="store_true",
+                   help="N>1: rank 0 re-renders every tile alone and checks the reduced film bit for bit")
     p.add_argument("--max-paths", type=int, default=0, help="paths per wavefront chunk (0 = library default)")
     a = p.parse_args()
     c = CONFIGS[a.config]
@@ -75,11 +80,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # RTG_DIST_BACKEND=gloo rehearses the N>1 path on one GPU (ranks share cuda:0, the film reduce
+    # goes through host memory); the default is RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("RTG_DIST_BACKEND", "nccl")
     if world > 1:
         import torch
         import torch.distributed as dist
+        ndev = max(1, torch.cuda.device_count())
+        local = local % ndev
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    coll_dev = "cuda:%d" % local if backend == "nccl" else "cpu"
 
     from raytracingrenderer_amd import RayTracer, loadScene, write_synthetic_scene
     from raytracingrenderer_amd import _native as N
@@ -98,17 +112,22 @@ def main():
     rt = RayTracer(scene, device=local, max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
     from raytracingrenderer_amd.distributed import reduce_film, tiles_for_rank
     tiles = tiles_for_rank(a.width, a.height, rank, world)
+    if a.shard_of > 1 and world == 1:
+        tiles = tiles_for_rank(a.width, a.height, 0, a.shard_of)
 
     film_t = None
     if world > 1:
         import torch
-        film_t = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device="cuda:%d" % local)
+        film_t = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=coll_dev)
 
     def step():
         rt.clear()
         rt.render(a.spp, tiles=tiles, first_sample=0)
         if world > 1:
-            rt.copy_film_to(film_t.data_ptr())
+            if backend == "nccl":
+                rt.copy_film_to(film_t.data_ptr())
+            else:
+                film_t.copy_(torch.from_numpy(rt.film()[0]))
             reduce_film(film_t, dist)
 
     def barrier_sync():
@@ -155,31 +174,50 @@ def main():
     cw = cs if a.bvh2 else count(base)
     rt.set_options(flags=base)
 
+    film_check = None
+    if world > 1 and a.verify_film:
+        step()  # a fresh reduced film
+        barrier_sync()
+        if rank == 0:
+            reduced = film_t.cpu().numpy() if backend == "nccl" else film_t.numpy()
+            rt.clear()
+            rt.render(a.spp, tiles=None, first_sample=0)
+            solo = rt.film()[0]
+            film_check = bool(np.array_equal(reduced.view(np.uint32), solo.view(np.uint32)))
+        barrier_sync()
+
     local_kernel_ms = (extend_ms, shadow_ms, shade_ms)
     totals = np.array([ext_rays, shadow_rays, paths, extend_ms, extend_launches,
                        cs["node_visits"], cs["tri_tests"], cs["extension_rays"],
-                       cw["node_visits"], cw["tri_tests"]], dtype=np.float64)
+                       cw["node_visits"], cw["tri_tests"],
+                       cs["shadow_node_visits"], cs["shadow_tri_tests"], cs["shadow_rays"]], dtype=np.float64)
     t_max = elapsed
     if world > 1:
         import torch
-        tt = torch.tensor(totals, dtype=torch.float64, device="cuda:%d" % local)
+        tt = torch.tensor(totals, dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.SUM)
         totals = tt.cpu().numpy()
-        te = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
+        te = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         t_max = float(te.item())
-    ext_rays, shadow_rays, paths, extend_ms, extend_launches, c_nodes, c_tris, c_ext, w_nodes, w_tris = totals.tolist()
+    (ext_rays, shadow_rays, paths, extend_ms, extend_launches, c_nodes, c_tris, c_ext, w_nodes, w_tris,
+     s_nodes, s_tris, c_sh) = totals.tolist()
     rays = ext_rays + shadow_rays
     mrays = rays / t_max / 1e6
     ms_step = t_max * 1e3 / a.steps
 
-    # roofline for the dominant kernel (closest-hit traversal): algorithmic bytes per ray
-    # B = 32 B x box tests + 36 B x triangle tests + 48 B ray I/O
+    # roofline for the dominant kernel, k_trace (one launch per bounce traces the extension rays of
+    # bounce b and the shadow rays of bounce b-1): algorithmic bytes per ray
+    # B = 32 B x box tests + 36 B x triangle tests + 48 B ray I/O, with the box and
+    # triangle tests of the reference's own walk (BVH2, counted on the same workload)
     boxes_per_ray = c_nodes / max(c_ext, 1)
     tris_per_ray = c_tris / max(c_ext, 1)
     b_ray = 32.0 * boxes_per_ray + 36.0 * tris_per_ray + 48.0
-    # per-rank average launch: ext rays and time both summed over ranks/launches
-    achieved_gbs = (b_ray * ext_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
+    s_boxes_per_ray = s_nodes / max(c_sh, 1)
+    s_tris_per_ray = s_tris / max(c_sh, 1)
+    b_sray = 32.0 * s_boxes_per_ray + 36.0 * s_tris_per_ray + 48.0
+    # time and rays both summed over ranks and launches
+    achieved_gbs = (b_ray * ext_rays + b_sray * shadow_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
     traffic = None
     if os.path.exists(PMC_SUMMARY):
         try:
@@ -210,33 +248,40 @@ def main():
             "dtype": "f32",
             "data": ("synthetic (splitmix64 random triangles, generated in-run)" if cfg["scene"] is None
                      else "reference scene assets (%s%s)" % (cfg["scene"], ", filtered" if cfg.get("skip_missing") else "")),
+            **({"shard_of": a.shard_of} if a.shard_of > 1 else {}),
             "config": {"workload": "%s: %s, %dx%d, %d spp, MAX_DEPTH %d" % (
                            a.config, "synth-1M" if cfg["scene"] is None else cfg["scene"] + ("_f" if cfg.get("skip_missing") else ""),
                            a.width, a.height, a.spp, a.max_depth),
                        "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
                        "max_depth": a.max_depth, "parallelism": "tile-sharded x%d + RCCL film reduce" % world},
-            "roofline": {"bound": "hbm", "kernel": "k_trace<closest>",
+            "roofline": {"bound": "hbm", "kernel": "k_trace (extension + shadow rays)",
                          "achieved": None if achieved_gbs is None else round(achieved_gbs, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": None if achieved_gbs is None else round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
                          "tri_tests_per_ray": round(tris_per_ray, 2),
+                         "bytes_per_shadow_ray": round(b_sray, 1),
+                         "shadow_box_tests_per_ray": round(s_boxes_per_ray, 2),
+                         "shadow_tri_tests_per_ray": round(s_tris_per_ray, 2),
+                         "limiter": "vector-memory address/L1 request rate (TA busy ~87 %); the scene is "
+                                    "served from L2/Infinity Cache, so algorithmic bytes can exceed the HBM "
+                                    "peak (DESIGN.md §4)",
                          "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from the reference BVH2)",
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
-                         "pops_per_ray": round(cw["pops"] / max(c_ext, 1), 2),
-                         "cullable_pops_per_ray": round(cw["cullable_pops"] / max(c_ext, 1), 2),
+                         "pops_per_ray": round(cw["pops"] / max(cw["extension_rays"], 1), 2),
+                         "cullable_pops_per_ray": round(cw["cullable_pops"] / max(cw["extension_rays"], 1), 2),
                          # node: lanes stepping a node per loop iteration; leaf: lanes running a
                          # parked leaf per leaf phase; leaf phases per iteration
                          "lane_util_node_leaf": [round(cw["node_lane_steps"] / max(cw["lane_slots"], 1), 3),
                                                  round(cw["leaf_lane_steps"] / max(cw["leaf_phase_slots"], 1), 3),
                                                  round(cw["leaf_phase_slots"] / max(cw["lane_slots"], 1), 3)],
                          "avg_launch_ms": round(extend_ms / max(extend_launches, 1), 4)},
-            "kernel_ms_per_step_rank0": {"closest_hit": round(local_kernel_ms[0] / a.steps, 2),
-                                         "any_hit": round(local_kernel_ms[1] / a.steps, 2),
+            "kernel_ms_per_step_rank0": {"trace": round(local_kernel_ms[0] / a.steps, 2),
                                          "generate_shade_accumulate": round(local_kernel_ms[2] / a.steps, 2)},
             "cpu_baseline": cpu,
+            **({"film_reduce_bit_exact": film_check} if film_check is not None else {}),
             "setup_s": round(setup_s, 2),
         }
         print(json.dumps(out), flush=True)

@@ -95,10 +95,11 @@ typedef struct rtg_stats {
     uint64_t tri_tests;            /* RTG_OPT_COUNT: triangle tests by closest-hit rays        */
     uint64_t shadow_node_visits;   /* RTG_OPT_COUNT: box tests by any-hit rays                 */
     uint64_t shadow_tri_tests;     /* RTG_OPT_COUNT: triangle tests by any-hit rays            */
-    uint64_t extend_launches;      /* RTG_OPT_TIMING: closest-hit launches in the last call    */
+    uint64_t extend_launches;      /* RTG_OPT_TIMING: traversal launches in the last call      */
     double   render_ms;            /* device time of the last rtg_render call                  */
-    double   extend_ms;            /* RTG_OPT_TIMING: closest-hit kernel time (last call)      */
-    double   shadow_ms;            /* device time spent in any-hit kernels (last call)         */
+    double   extend_ms;            /* RTG_OPT_TIMING: traversal kernel time, extension + shadow */
+                                   /* rays (one k_trace launch per bounce; last call)          */
+    double   shadow_ms;            /* unused since shadow rays share the traversal launches (0) */
     double   shade_ms;             /* device time spent in generate/shade/accumulate kernels   */
     uint64_t lane_slots;           /* RTG_OPT_COUNT: closest-hit loop iterations x 64 lanes     */
     uint64_t node_lane_steps;      /* RTG_OPT_COUNT: lanes doing a node step, summed            */

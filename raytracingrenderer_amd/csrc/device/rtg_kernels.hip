@@ -4,13 +4,14 @@
 // ns samples x npix pixels = P paths in flight, advanced bounce by bounce:
 //
 //   k_generate        Camera::generateRay (Scene.h:43-54) at pixel centres, PCG32 seed, path state
-//   for b in 0 .. max_depth+1:                                   (pathTrace recursion, depth = b)
-//     k_trace<closest> Scene::traverse  (Scene.h:107-130, Geometry.h:399-434)
-//     k_shade          calculateShadingData + emission + computeDirect (NEE sample, shadow ray)
-//                      + Russian roulette + BSDF::sample + throughput (Renderer.h:328-392, 423-473)
-//                      -> compacts continuing paths into the next extension queue and NEE rays
-//                      into the shadow queue (wave ballot + mbcnt prefix, one atomic per wave)
-//     k_trace<any>     Scene::visible   (Scene.h:161-169, Geometry.h:435-462)
+//   for b in 0 .. max_depth+2:                                   (pathTrace recursion, depth = b)
+//     k_shade (b > 0)  bounce b-1: calculateShadingData + emission + computeDirect (NEE sample,
+//                      shadow ray) + Russian roulette + BSDF::sample + throughput
+//                      (Renderer.h:328-392, 423-473) -> compacts continuing paths into the next
+//                      extension queue and NEE rays into the shadow queue (one atomic per block)
+//     k_trace          one launch for both ray kinds: Scene::traverse (Scene.h:107-130,
+//                      Geometry.h:399-434) for the extension rays of bounce b and Scene::visible
+//                      (Scene.h:161-169, Geometry.h:435-462) for the shadow rays of bounce b-1
 //   k_accumulate      right-nested radiance sum d0 + (d1 + (... + dk)) (Renderer.h:388) per path,
 //                      then film += L in sample order (Film::splat, Imaging.h:209-232)
 //
@@ -58,16 +59,22 @@ struct __align__(16) Counters { unsigned n_ext, n_shadow, f_ext, f_shadow, f_sha
 
 // Queues hold path ids only; ray payloads live in per-path arrays (written in place by k_shade),
 // so compaction moves 4 bytes per ray and needs one atomic per 256 paths.
+// One traversal launch serves two ray sets: extension (closest-hit) rays take work indices
+// [0, nc) and NEE shadow (any-hit) rays [nc, nc + ns). Each lane carries its ray's kind.
 struct TraceIO {
-    const unsigned* queue;     // path ids to trace
-    const float4* ray_o;       // [pid] origin.xyz, w = maxT (any-hit)
-    const float4* ray_d;       // [pid] direction.xyz
-    const float4* ray_c;       // [pid] any-hit: NEE value copied to contrib[pid] when visible
-    const unsigned* count;     // number of rays (device)
-    unsigned* fetch;           // work counter (device, zeroed)
+    const unsigned* queue;     // closest: path ids to trace
+    const float4* ray_o;       // closest: [pid] origin.xyz
+    const float4* ray_d;       // closest: [pid] direction.xyz
+    const unsigned* count;     // closest: number of rays (device; null = none)
     float4* hits;              // closest-hit output [pid]
+    const unsigned* squeue;    // any-hit: path ids
+    const float4* sray_o;      // any-hit: [pid] origin.xyz, w = maxT
+    const float4* sray_d;      // any-hit: [pid] direction.xyz
+    const float4* sray_c;      // any-hit: [pid] NEE value copied to contrib[pid] when visible
+    const unsigned* scount;    // any-hit: number of rays (device; null = none)
     float4* contrib;           // any-hit: this bounce's contribution plane [pid]
     int* visible;              // any-hit query output [pid] (instead of contrib)
+    unsigned* fetch;           // work counter over both sets (device, zeroed)
     int* ovf;                  // global stack overflow [level][thread]
     unsigned long long* stats; // [0,1] closest / [4,5] any-hit: box tests, triangle tests (COUNT)
     int cull;
@@ -109,7 +116,7 @@ static __device__ __forceinline__ unsigned prefix_lt(unsigned long long m) {
 // queue (one atomic per 64 rays) into a wave-uniform pool, and every lane whose ray terminates
 // immediately takes the next index from the pool. Without replacement a wave runs until its
 // longest ray finishes (measured SIMD efficiency ~27 %).
-template <bool ANY, bool COUNT>
+template <bool COUNT>
 __global__ __launch_bounds__(RTG_TB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
 void k_trace(SceneView s, TraceIO io) {
     __shared__ int stk[RTG_STACK][RTG_TB];
@@ -118,8 +125,10 @@ void k_trace(SceneView s, TraceIO io) {
     const int lane = lane_id();
     const unsigned gthreads = gridDim.x * blockDim.x;
     const unsigned gtid = blockIdx.x * blockDim.x + tid;
-    const unsigned n = *io.count;
-    unsigned long long c_nodes = 0, c_tris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0, c_cullpop = 0, c_pops = 0, c_lslots = 0;
+    const unsigned nc = io.count ? *io.count : 0u;
+    const unsigned n = nc + (io.scount ? *io.scount : 0u);
+    unsigned long long c_nodes = 0, c_tris = 0, c_snodes = 0, c_stris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0,
+                       c_cullpop = 0, c_pops = 0, c_lslots = 0;
     unsigned pool_base = 0, pool_left = 0;  // wave-uniform
     bool drained = false;                   // wave-uniform
     bool have = false;
@@ -127,13 +136,13 @@ void k_trace(SceneView s, TraceIO io) {
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tbest = 0.0f, omag = 0.0f, dmag = 0.0f, delta = 0.0f, bu = 0.0f, bv = 0.0f;
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0, pend = RTG_EXIT;
-    bool occluded = false, wide = false;
+    bool occluded = false, wide = false, anyr = false;  // anyr: this lane's ray is a shadow ray
     for (;;) {
         // ---- retire finished rays
         if (have && cur == RTG_EXIT && pend == RTG_EXIT) {
-            if (ANY) {
+            if (anyr) {
                 if (io.visible) io.visible[pid] = occluded ? 0 : 1;
-                else if (!occluded) io.contrib[pid] = io.ray_c[pid];
+                else if (!occluded) io.contrib[pid] = io.sray_c[pid];
             } else {
                 io.hits[pid] = make_float4(tbest, __int_as_float(bid), bu, bv);
             }
@@ -159,11 +168,13 @@ void k_trace(SceneView s, TraceIO io) {
                 if (!have && pos < take) {
                     ri = pool_base + pos;
                     have = true;
-                    pid = (int)io.queue[ri];
-                    const float4 ro = io.ray_o[pid], rd = io.ray_d[pid];
+                    anyr = ri >= nc;
+                    pid = (int)(anyr ? io.squeue[ri - nc] : io.queue[ri]);
+                    const float4 ro = anyr ? io.sray_o[pid] : io.ray_o[pid];
+                    const float4 rd = anyr ? io.sray_d[pid] : io.ray_d[pid];
                     o = mk(ro.x, ro.y, ro.z);
                     d = mk(rd.x, rd.y, rd.z);
-                    tbest = ANY ? ro.w : RTG_FLT_MAX;
+                    tbest = anyr ? ro.w : RTG_FLT_MAX;
                     inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // Ray::init
                     omag = s.cull_scale + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
                     dmag = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
@@ -188,7 +199,7 @@ void k_trace(SceneView s, TraceIO io) {
             }
         }
         if (drained && __ballot(have) == 0) break;
-        if (COUNT && !ANY) {
+        if (COUNT) {
             c_slots += 64;
             c_nstep += (have && cur >= 0) ? 1 : 0;
             if (!RTG_POSTPONE) c_lstep += (have && cur != RTG_EXIT && cur < 0) ? 1 : 0;
@@ -202,12 +213,12 @@ void k_trace(SceneView s, TraceIO io) {
             bool lchk = false, lok = true;  // exact leaf box, tested on the first candidate only
             for (int k = 0; k < cnt; ++k) {
                 const int tri = start + k;
-                if (COUNT) c_tris += 1;
+                if (COUNT) (anyr ? c_stris : c_tris) += 1;
                 const DevTri T = s.tris[tri];
                 float t, u, v;
                 if (tri_intersect(T, o, d, t, u, v)) {
-                    bool cand = ANY ? !(t >= tbest || t <= RTG_EPS)
-                                    : (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid)));
+                    bool cand = anyr ? !(t >= tbest || t <= RTG_EPS)
+                                     : (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid)));
 #if RTG_QNODE
                     if (cand && wide) {
                         if (!lchk) {
@@ -219,7 +230,7 @@ void k_trace(SceneView s, TraceIO io) {
                     }
 #endif
                     if (!cand) {
-                    } else if (ANY) {
+                    } else if (anyr) {
                         occluded = true;
                     } else {
                         tbest = t;
@@ -296,7 +307,7 @@ void k_trace(SceneView s, TraceIO io) {
                         // (finite here, so a miss is the only +inf key)
                         // (bitwise & / |: no branches per slot)
                         const bool hit = (wd[k + j] != RTG_EXIT) & !((tx < en) | (tx < 0.0f)) & (!io.cull | !(e > tbest));
-                        if (COUNT) c_nodes += wd[k + j] != RTG_EXIT ? 1 : 0;
+                        if (COUNT) (anyr ? c_snodes : c_nodes) += wd[k + j] != RTG_EXIT ? 1 : 0;
                         key[k + j] = hit ? e : __builtin_inff();
                     }
                 }
@@ -327,7 +338,7 @@ void k_trace(SceneView s, TraceIO io) {
                 bool hit = wd[k] != RTG_EXIT && slab_exact(mnx, mny, mnz, mxx, mxy, mxz, o, inv);
                 const float e = slab_cull_entry(mnx, mny, mnz, mxx, mxy, mxz, o, inv, delta);
                 if (io.cull) hit = hit && !(e > tbest);
-                if (COUNT) c_nodes += wd[k] != RTG_EXIT ? 1 : 0;
+                if (COUNT) (anyr ? c_snodes : c_nodes) += wd[k] != RTG_EXIT ? 1 : 0;
                 key[k] = hit ? fmaxf(e, -RTG_FLT_MAX) : __builtin_inff();
             }
 #endif
@@ -364,7 +375,7 @@ void k_trace(SceneView s, TraceIO io) {
                 cur = wd[0];
             }
         } else if (cur >= 0) {
-            if (COUNT) c_nodes += 2;
+            if (COUNT) (anyr ? c_snodes : c_nodes) += 2;
             const DevNode nd = s.nodes[cur];
             bool hl = slab_exact(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, o, inv);
             bool hr = slab_exact(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, o, inv);
@@ -400,19 +411,19 @@ void k_trace(SceneView s, TraceIO io) {
 #else
         else if (cur != RTG_EXIT) {
             leaf(cur);
-            cur = (ANY && occluded) ? RTG_EXIT : RTG_POP;
+            cur = (anyr && occluded) ? RTG_EXIT : RTG_POP;
         }
 #endif
         // ---- one pop for every branch: always an LDS read (ds_read, not a flat load through a
         // selected pointer); the global overflow read only for deep entries
         if (cur == RTG_POP) {
-            if (COUNT && !ANY && sp > 0) c_pops += 1;
+            if (COUNT && !anyr && sp > 0) c_pops += 1;
             if (sp == 0) {
                 cur = RTG_EXIT;
             } else {
                 --sp;
                 cur = stk[sp < RTG_STACK ? sp : 0][tid];
-                if (COUNT && !ANY && sp < RTG_STACK && kstk[sp][tid] > tbest) c_cullpop += 1;
+                if (COUNT && !anyr && sp < RTG_STACK && kstk[sp][tid] > tbest) c_cullpop += 1;
                 if (sp >= RTG_STACK) cur = io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
             }
         }
@@ -420,14 +431,14 @@ void k_trace(SceneView s, TraceIO io) {
         // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on
         const unsigned long long pm = __ballot(pend != RTG_EXIT);
         if (__popcll(pm) >= RTG_POSTPONE || __ballot(cur >= 0) == 0) {
-            if (COUNT && !ANY) {
+            if (COUNT) {
                 c_lslots += 64;
                 c_lstep += pend != RTG_EXIT ? 1 : 0;
             }
             if (pend != RTG_EXIT) {
                 leaf(pend);
                 pend = RTG_EXIT;
-                if (ANY && occluded) {
+                if (anyr && occluded) {
                     cur = RTG_EXIT;
                     sp = 0;
                 }
@@ -439,22 +450,24 @@ void k_trace(SceneView s, TraceIO io) {
         for (int off = 32; off > 0; off >>= 1) {
             c_nodes += __shfl_down(c_nodes, off);
             c_tris += __shfl_down(c_tris, off);
+            c_snodes += __shfl_down(c_snodes, off);
+            c_stris += __shfl_down(c_stris, off);
             c_nstep += __shfl_down(c_nstep, off);
             c_lstep += __shfl_down(c_lstep, off);
             c_cullpop += __shfl_down(c_cullpop, off);
             c_pops += __shfl_down(c_pops, off);
         }
         if (lane == 0) {
-            atomicAdd(&io.stats[ANY ? 4 : 0], c_nodes);
-            atomicAdd(&io.stats[ANY ? 5 : 1], c_tris);
-            if (!ANY) {
-                atomicAdd(&io.stats[8], c_slots);
-                atomicAdd(&io.stats[9], c_nstep);
-                atomicAdd(&io.stats[10], c_lstep);
-                atomicAdd(&io.stats[13], c_lslots);
-                atomicAdd(&io.stats[11], c_cullpop);
-                atomicAdd(&io.stats[12], c_pops);
-            }
+            atomicAdd(&io.stats[0], c_nodes);
+            atomicAdd(&io.stats[1], c_tris);
+            atomicAdd(&io.stats[4], c_snodes);
+            atomicAdd(&io.stats[5], c_stris);
+            atomicAdd(&io.stats[8], c_slots);
+            atomicAdd(&io.stats[9], c_nstep);
+            atomicAdd(&io.stats[10], c_lstep);
+            atomicAdd(&io.stats[13], c_lslots);
+            atomicAdd(&io.stats[11], c_cullpop);
+            atomicAdd(&io.stats[12], c_pops);
         }
     }
 }
@@ -1173,14 +1186,11 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     for (auto& e : h->ev) HIPOK(hipEventCreate(&e));
 
     int occ = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false, false>, RTG_TB, 0));
-    int occ2 = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_trace<true, false>, RTG_TB, 0));
-    h->trace_blocks = h->n_cu * std::max(1, std::max(occ, occ2));
-    int occ3 = 0, occ4 = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_trace<false, true>, RTG_TB, 0));
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ4, k_trace<true, true>, RTG_TB, 0));
-    h->trace_blocks_count = h->n_cu * std::max(1, std::max(occ3, occ4));
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false>, RTG_TB, 0));
+    h->trace_blocks = h->n_cu * std::max(1, occ);
+    int occ3 = 0;
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_trace<true>, RTG_TB, 0));
+    h->trace_blocks_count = h->n_cu * std::max(1, occ3);
     int occs = 0;
     HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occs, k_shade, RTG_TB, 0));
     h->shade_blocks = h->n_cu * std::max(1, occs);
@@ -1310,36 +1320,33 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
         hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, h->pb);
         LAUNCH_OK("k_generate");
         timed_end(h, st, k); kinds.push_back(2); ++k;
-        for (int b = 0; b < maxb; ++b) {
+        // Trace launch L_b (b = 0..maxb) carries the extension rays of bounce b (from shade(b-1),
+        // or generate) and the shadow rays of bounce b-1: one persistent launch, one drain tail.
+        for (int b = 0; b <= maxb; ++b) {
+            if (b > 0) {
+                timed_begin(h, st, k);
+                hipLaunchKernelGGL(k_shade, dim3(h->shade_blocks), dim3(RTG_TB), 0, st, h->sv, a, h->pb, b - 1);
+                LAUNCH_OK("k_shade");
+                timed_end(h, st, k); kinds.push_back(2); ++k;
+            }
             io.queue = h->pb.q[b & 1];
             io.ray_o = h->pb.ray_o;
             io.ray_d = h->pb.ray_d;
-            io.count = &h->pb.ctr[b].n_ext;
-            io.fetch = &h->pb.ctr[b].f_ext;
+            io.count = b < maxb ? &h->pb.ctr[b].n_ext : nullptr;
             io.hits = h->pb.hits;
+            io.squeue = h->pb.shq;
+            io.sray_o = h->pb.sh_o;
+            io.sray_d = h->pb.sh_d;
+            io.sray_c = h->pb.sh_c;
+            io.scount = b > 0 ? &h->pb.ctr[b - 1].n_shadow : nullptr;
+            io.contrib = b > 0 ? h->pb.contrib + (size_t)(b - 1) * a.P : nullptr;
+            io.visible = nullptr;
+            io.fetch = &h->pb.ctr[b].f_ext;
             timed_begin(h, st, k);
-            if (h->count) hipLaunchKernelGGL((k_trace<false, true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
-            else hipLaunchKernelGGL((k_trace<false, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
-            LAUNCH_OK("k_trace<closest>");
+            if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
+            else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
+            LAUNCH_OK("k_trace");
             timed_end(h, st, k); kinds.push_back(0); ++k;
-            timed_begin(h, st, k);
-            hipLaunchKernelGGL(k_shade, dim3(h->shade_blocks), dim3(RTG_TB), 0, st, h->sv, a, h->pb, b);
-            LAUNCH_OK("k_shade");
-            timed_end(h, st, k); kinds.push_back(2); ++k;
-            TraceIO sio = io;
-            sio.queue = h->pb.shq;
-            sio.ray_o = h->pb.sh_o;
-            sio.ray_d = h->pb.sh_d;
-            sio.ray_c = h->pb.sh_c;
-            sio.count = &h->pb.ctr[b].n_shadow;
-            sio.fetch = &h->pb.ctr[b].f_shadow;
-            sio.contrib = h->pb.contrib + (size_t)b * a.P;
-            sio.visible = nullptr;
-            timed_begin(h, st, k);
-            if (h->count) hipLaunchKernelGGL((k_trace<true, true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, sio);
-            else hipLaunchKernelGGL((k_trace<true, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, sio);
-            LAUNCH_OK("k_trace<any>");
-            timed_end(h, st, k); kinds.push_back(1); ++k;
         }
         hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, st, h->pb.ctr, maxb, h->d_stats);
         LAUNCH_OK("k_tally");
@@ -1475,22 +1482,25 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
     int rc = ensure_ovf(h);
     if (rc) return rc;
     TraceIO io{};
-    io.count = h->d_qctr;
     io.fetch = h->d_qctr + 1;
     io.ovf = h->d_ovf;
     io.stats = h->d_stats;
     io.cull = h->cull;
     io.wide = h->wide;
-    io.queue = d_q;
-    io.ray_o = d_o;
-    io.ray_d = d_d;
     if (any) {
+        io.squeue = d_q;
+        io.sray_o = d_o;
+        io.sray_d = d_d;
+        io.scount = h->d_qctr;
         io.visible = (int*)d_out;
-        hipLaunchKernelGGL((k_trace<true, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, io);
     } else {
+        io.queue = d_q;
+        io.ray_o = d_o;
+        io.ray_d = d_d;
+        io.count = h->d_qctr;
         io.hits = (float4*)d_out;
-        hipLaunchKernelGGL((k_trace<false, false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, io);
     }
+    hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, io);
     HIPOK(hipGetLastError());
     HIPOK(hipStreamSynchronize(h->stream));
     if (any) HIPOK(hipMemcpy(vis, d_out, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));

@@ -31,7 +31,7 @@ def main(fetch_csv, write_csv, stats_csv, out_json, dram_csv=None):
         if k in rq and sum(rq[k]) > 0:
             # share of L2 read requests that went to DRAM (the rest hit the Infinity Cache)
             out["kernels"][k]["dram_share_of_l2_read_requests"] = round(sum(rd.get(k, [0])) / sum(rq[k]), 4)
-    ext = [k for k in out["kernels"] if k.startswith("void k_trace<false, false>")]
+    ext = [k for k in out["kernels"] if k.startswith("void k_trace<false>") or k.startswith("void k_trace<false, false>")]
     if ext:
         e = out["kernels"][ext[0]]
         out["extend_l2_fabric_bytes_per_launch"] = e["read_bytes_corrected"] + e["write_bytes"]
