@@ -259,6 +259,11 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": None if achieved_gbs is None else round(achieved_gbs / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
+                         # L2->fabric bytes per launch (PMC, profiles/) over this run's average launch
+                         "traffic_gbs": (round(traffic / (extend_ms / max(extend_launches, 1) / 1e3) / 1e9, 1)
+                                         if traffic and extend_ms > 0 else None),
+                         "traffic_frac": (round(traffic / (extend_ms / max(extend_launches, 1) / 1e3) / 1e9
+                                                / HBM_PEAK_GBS, 4) if traffic and extend_ms > 0 else None),
                          "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
                          "tri_tests_per_ray": round(tris_per_ray, 2),
                          "bytes_per_shadow_ray": round(b_sray, 1),
