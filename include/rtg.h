@@ -132,6 +132,17 @@ void rtg_destroy(rtg_handle* h);
 #define RTG_OPT_BVH2   8
 int  rtg_set_options(rtg_handle* h, int max_depth, int flags, uint32_t max_paths_in_flight);
 
+/* Per-pixel estimator (the alternative RayTracer methods of Renderer.h). PATH is RayTracer::render's
+ * pathTrace (Renderer.h:328-392, the default). DIRECT = RayTracer::direct (:393-407): emission or one
+ * NEE sample at the first hit, 0 on a miss. ALBEDO = RayTracer::albedo (:558-571): emission,
+ * BSDF::evaluate(sd, (0,1,0)) or the background. NORMALS = RayTracer::viewNormals (:572-582):
+ * |shading normal| at the first hit. */
+#define RTG_INTEGRATOR_PATH    0
+#define RTG_INTEGRATOR_DIRECT  1
+#define RTG_INTEGRATOR_ALBEDO  2
+#define RTG_INTEGRATOR_NORMALS 3
+int  rtg_set_integrator(rtg_handle* h, int integrator);
+
 /* Add samples [first_sample, first_sample+n_samples) of every pixel in the listed 32x32 tiles
  * (tile id = ty*tilesX + tx, RTBase TILE_SIZE=32; tile_ids=NULL = all tiles) to the film, in
  * sample order per pixel. Equivalent to n_samples calls of RayTracer::render() with the

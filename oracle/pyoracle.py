@@ -23,6 +23,7 @@ def lib(flavour="rtm"):
         L.or_create.argtypes = [vp, C.c_int]
         L.or_destroy.argtypes = [vp]
         L.or_set_max_depth.argtypes = [vp, C.c_int]
+        L.or_set_integrator.argtypes = [vp, C.c_int]
         L.or_render.restype = C.c_int
         L.or_render.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32, C.c_int, f32p,
                                 C.POINTER(C.c_uint64), C.c_int]
@@ -44,12 +45,13 @@ def _p(a, t):
 
 
 class Oracle:
-    def __init__(self, scene, max_depth=4, flavour="rtm"):
+    def __init__(self, scene, max_depth=4, flavour="rtm", integrator=0):
         self.L = lib(flavour)
         self.scene = scene  # keeps the desc alive
         self.h = self.L.or_create(C.cast(scene.desc_ptr, C.c_void_p), max_depth)
         if not self.h:
             raise RuntimeError("or_create failed")
+        self.L.or_set_integrator(self.h, integrator)
         self.W, self.H = scene.width, scene.height
 
     def __del__(self):

@@ -127,7 +127,7 @@ typedef struct { V3 mn, mx; int l, r, start, end; } Node;
 typedef struct { int w, h; const float* t; } Tex;
 
 struct or_scene {
-    int ntri, nnode, nlight, env_tex, max_depth;
+    int ntri, nnode, nlight, env_tex, max_depth, integrator;
     Tri* tri;
     Node* node;
     rtg_material* mat;
@@ -458,13 +458,54 @@ static Ray camera_ray(const struct or_scene* s, float x, float y) {
     return ray_make(v3(c->origin[0], c->origin[1], c->origin[2]), d);
 }
 
+/* RayTracer::direct (Renderer.h:393-407): emission or one NEE sample at the first hit; 0 on a miss */
+static Col direct_only(const struct or_scene* s, Ray* r, Pcg* smp, Counts* c) {
+    Isect is = scene_traverse(s, r, c);
+    Shading sd = shading_data(s, &is, r);
+    if (sd.t < FLT_MAX) {
+        if (is_light(sd.bsdf)) return col(sd.bsdf->emission[0], sd.bsdf->emission[1], sd.bsdf->emission[2]);
+        return compute_direct(s, &sd, smp, c);
+    }
+    return col(0.0f, 0.0f, 0.0f);
+}
+
+/* RayTracer::albedo (Renderer.h:558-571): emission, BSDF::evaluate(sd, (0,1,0)) or background */
+static Col albedo_only(const struct or_scene* s, Ray* r, Counts* c) {
+    Isect is = scene_traverse(s, r, c);
+    Shading sd = shading_data(s, &is, r);
+    if (sd.t < FLT_MAX) {
+        const rtg_material* m = sd.bsdf;
+        if (is_light(m)) return col(m->emission[0], m->emission[1], m->emission[2]);
+        if (m->kind == RTG_MAT_MIRROR) return tex_sample(s, m->texture, sd.tu, sd.tv); /* Materials.h:178-183 */
+        if (m->kind == RTG_MAT_GLASS) return col(0.0f, 0.0f, 0.0f);
+        return bsdf_eval(s, &sd);
+    }
+    if (s->env_tex < 0) return col(0.0f, 0.0f, 0.0f);
+    return env_eval(s, r->dir);
+}
+
+/* RayTracer::viewNormals (Renderer.h:572-582): |shading normal| at the first hit */
+static Col normals_only(const struct or_scene* s, Ray* r, Counts* c) {
+    Isect is = scene_traverse(s, r, c);
+    if (is.t < FLT_MAX) {
+        Shading sd = shading_data(s, &is, r);
+        return col(fabsf(sd.sN.x), fabsf(sd.sN.y), fabsf(sd.sN.z));
+    }
+    return col(0.0f, 0.0f, 0.0f);
+}
+
 static Col pixel_sample(const struct or_scene* s, uint32_t pixel, uint32_t sample, uint64_t seed, Counts* c) {
     uint32_t x = pixel % (uint32_t)s->W, y = pixel / (uint32_t)s->W;
     Pcg smp;
     pcg_init(&smp, seed, ((uint64_t)pixel << 16) | sample);
     Ray r = camera_ray(s, x + 0.5f, y + 0.5f);
     Col thr = col(1.0f, 1.0f, 1.0f);
-    return path_trace(s, &r, &thr, 0, &smp, 1, c);
+    switch (s->integrator) {
+    case RTG_INTEGRATOR_DIRECT: return direct_only(s, &r, &smp, c);
+    case RTG_INTEGRATOR_ALBEDO: return albedo_only(s, &r, c);
+    case RTG_INTEGRATOR_NORMALS: return normals_only(s, &r, c);
+    default: return path_trace(s, &r, &thr, 0, &smp, 1, c);
+    }
 }
 
 /* ------------------------------------------------------------------ public C API (ctypes) */
@@ -536,6 +577,7 @@ void or_destroy(or_scene* s) {
 }
 
 void or_set_max_depth(or_scene* s, int max_depth) { if (s) s->max_depth = max_depth; }
+void or_set_integrator(or_scene* s, int integrator) { if (s) s->integrator = integrator; }
 
 /* Per-path radiance for an explicit (pixel, sample) list: out n*3. */
 int or_trace_paths(or_scene* s, const uint32_t* pixels, const uint32_t* samples, uint32_t n, uint64_t seed, float* out) {

@@ -11,6 +11,7 @@ LIB_DIR = os.path.join(_HERE, "lib")
 
 RTG_MAT_DIFFUSE, RTG_MAT_LAMBERT, RTG_MAT_MIRROR, RTG_MAT_GLASS = 0, 1, 2, 3
 RTG_OPT_CULL, RTG_OPT_COUNT, RTG_OPT_TIMING, RTG_OPT_BVH2 = 1, 2, 4, 8
+RTG_INTEGRATOR_PATH, RTG_INTEGRATOR_DIRECT, RTG_INTEGRATOR_ALBEDO, RTG_INTEGRATOR_NORMALS = 0, 1, 2, 3
 
 f32p = C.POINTER(C.c_float)
 u32p = C.POINTER(C.c_uint32)
@@ -69,6 +70,7 @@ RTG_EXPORTS = [
     ("rtg_create", C.c_int, [C.c_int, C.POINTER(rtg_scene_desc), C.POINTER(C.c_void_p)]),
     ("rtg_destroy", None, [C.c_void_p]),
     ("rtg_set_options", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_uint32]),
+    ("rtg_set_integrator", C.c_int, [C.c_void_p, C.c_int]),
     ("rtg_render", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32]),
     ("rtg_render_async", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32, C.c_void_p]),
     ("rtg_synchronize", C.c_int, [C.c_void_p]),

@@ -86,6 +86,7 @@ struct ChunkArgs {
     unsigned npix, ns, s0, P;
     unsigned long long seed;
     int max_depth;
+    int mode;                  // RTG_INTEGRATOR_* (first-hit estimators never continue a path)
     DevCamera cam;
 };
 
@@ -533,8 +534,10 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             v3 c;
             int nterms = b + 1;
             if (!(h.x < RTG_FLT_MAX)) {
-                // miss: background->evaluate(r.dir), not weighted by throughput (Renderer.h:390)
-                c = background(s, d);
+                // miss: background->evaluate(r.dir), not weighted by throughput (Renderer.h:390);
+                // direct() and viewNormals() return black
+                c = (a.mode == RTG_INTEGRATOR_PATH || a.mode == RTG_INTEGRATOR_ALBEDO) ? background(s, d)
+                                                                                     : mk(0.0f, 0.0f, 0.0f);
             } else {
                 const int tri = __float_as_int(h.y);
                 const float alpha = h.z, beta = h.w, gamma = 1.0f - (alpha + beta);
@@ -549,8 +552,14 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                 const v3 wo = neg(d);
                 if (M.two_sided && dot(wo, sn) < 0) sn = neg(sn);
                 const frame fr = frame_from(sn);
-                if (M.is_light) {
-                    c = can_hit ? mul(thr, mk(M.emission.x, M.emission.y, M.emission.z)) : mk(0.0f, 0.0f, 0.0f);
+                if (a.mode == RTG_INTEGRATOR_NORMALS) {  // viewNormals (Renderer.h:572-582)
+                    c = mk(fabsf(sn.x), fabsf(sn.y), fabsf(sn.z));
+                } else if (M.is_light) {
+                    c = a.mode != RTG_INTEGRATOR_PATH ? mk(M.emission.x, M.emission.y, M.emission.z)  // emit()
+                        : can_hit ? mul(thr, mk(M.emission.x, M.emission.y, M.emission.z)) : mk(0.0f, 0.0f, 0.0f);
+                } else if (a.mode == RTG_INTEGRATOR_ALBEDO) {  // BSDF::evaluate(sd, (0,1,0))
+                    const v3 alb = tex_sample(s, M.tex, tu, tv);
+                    c = M.kind == RTG_MAT_MIRROR ? alb : (M.kind == RTG_MAT_GLASS ? mk(0.0f, 0.0f, 0.0f) : divs(alb, RTG_PI_F));
                 } else {
                     const bool spec = M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS;
                     // ---- computeDirect (Renderer.h:423-473)
@@ -604,7 +613,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                     }
                     // direct = thr * Ld, with Ld = 0 until the shadow ray says visible
                     c = mul(thr, mk(0.0f, 0.0f, 0.0f));
-                    if (b <= a.max_depth) {
+                    if (a.mode == RTG_INTEGRATOR_PATH && b <= a.max_depth) {
                         const float rrp = wmin(lum(thr), 0.9f);
                         if (pcg_next(st, inc) < rrp) {
                             thr = divs(thr, rrp);
@@ -756,6 +765,7 @@ struct rtg_handle {
     DevNodeQ* d_nodesq = nullptr;
     float4* d_leafbox = nullptr;
     int usew = 0, wide = 1;
+    int integrator = RTG_INTEGRATOR_PATH;
     uint32_t wide_depth = 0;  // wide levels on the longest root-to-leaf path
     DevTri* d_tris = nullptr;
     DevShade* d_shade = nullptr;
@@ -1223,6 +1233,15 @@ void rtg_destroy(rtg_handle* h) {
     delete h;
 }
 
+int rtg_set_integrator(rtg_handle* h, int integrator) {
+    if (!h || integrator < RTG_INTEGRATOR_PATH || integrator > RTG_INTEGRATOR_NORMALS) {
+        g_err = "rtg_set_integrator: bad argument";
+        return RTG_ERR_ARG;
+    }
+    h->integrator = integrator;
+    return RTG_OK;
+}
+
 int rtg_set_options(rtg_handle* h, int max_depth, int cull, uint32_t max_paths) {
     if (!h || max_depth < 0 || max_depth > 250) { g_err = "rtg_set_options: bad argument"; return RTG_ERR_ARG; }
     h->max_depth = max_depth;
@@ -1314,6 +1333,7 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
         a.P = a.ns * h->npix;
         a.seed = seed;
         a.max_depth = h->max_depth;
+        a.mode = h->integrator;
         a.cam = h->cam;
         HIPOK(hipMemsetAsync(h->pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), st));
         timed_begin(h, st, k);

@@ -154,7 +154,11 @@ class RayTracer:
 
     MAX_DEPTH = 4  # Renderer.h:20
 
-    def __init__(self, scene, device=0, max_depth=MAX_DEPTH, seed=1234, cull=True, max_paths=0, wide=True):
+    INTEGRATORS = {"path": N.RTG_INTEGRATOR_PATH, "direct": N.RTG_INTEGRATOR_DIRECT,
+                   "albedo": N.RTG_INTEGRATOR_ALBEDO, "normals": N.RTG_INTEGRATOR_NORMALS}
+
+    def __init__(self, scene, device=0, max_depth=MAX_DEPTH, seed=1234, cull=True, max_paths=0, wide=True,
+                 integrator="path"):
         self.scene = scene
         self.seed = seed
         self._lib = N.rtg()
@@ -165,6 +169,14 @@ class RayTracer:
         self.max_depth = max_depth
         self.flags = (N.RTG_OPT_CULL if cull else 0) | (0 if wide else N.RTG_OPT_BVH2)
         self.set_options(max_depth=max_depth, flags=self.flags, max_paths=max_paths)
+        self.set_integrator(integrator)
+
+    def set_integrator(self, integrator):
+        """Per-pixel estimator: "path" (pathTrace, default), "direct", "albedo", "normals"
+        (RayTracer::direct / albedo / viewNormals, Renderer.h:393-407, 558-582)."""
+        mode = self.INTEGRATORS[integrator] if isinstance(integrator, str) else int(integrator)
+        _check(self._lib.rtg_set_integrator(self._h, mode), self._lib.rtg_last_error)
+        self.integrator = integrator
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None

@@ -230,6 +230,18 @@ def test_bathroom_filtered_crop_depth16():
                     "bathroom_f depth 16")
 
 
+@pytest.mark.parametrize("integrator", ["direct", "albedo", "normals"])
+def test_alternative_integrators(integrator):
+    """RayTracer::direct / albedo / viewNormals (Renderer.h:393-407, 558-582) on the mixed-material
+    scene (area + env lights, glass, mirror, two-sided Lambert stubs)."""
+    s = loadScene(os.path.join(SCENES, "cornell-mat"), width=80, height=60)
+    rt = RayTracer(s, seed=7, integrator=integrator)
+    rt.render(3, first_sample=0)
+    mode = RayTracer.INTEGRATORS[integrator]
+    ref, _ = Oracle(s, 4, "rtm", integrator=mode).render(3, seed=7, threads=8)
+    assert_bitexact(rt.film()[0], ref, integrator)
+
+
 def test_scene_without_lights_is_rejected(tmp_path):
     src = os.path.relpath(os.path.join(SCENES, "cornell-box"), str(tmp_path))
     (tmp_path / "scene.json").write_text(
