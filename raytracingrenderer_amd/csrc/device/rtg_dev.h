@@ -120,6 +120,17 @@ struct __align__(16) DevTri {
     float4 v2;    // vertices[2].p, -
     float4 e2;    // e2 = v0 - v2, -   (e1 = v2 - v1 is recomputed: same float op)
 };
+// Compact intersection record (48 B, three dwordx4 loads): n and the three vertices. d, e1, e2
+// and invArea are recomputed with Triangle::init's own float ops (Geometry.h:72-83), so they are
+// the same bits as the 64-B record's stored values.
+#ifndef RTG_TRI48
+#define RTG_TRI48 1
+#endif
+struct __align__(16) DevTri48 {
+    float4 a;  // n.xyz, v0.x
+    float4 b;  // v0.yz, v1.xy
+    float4 c;  // v1.z, v2.xyz
+};
 // Cold shading record (64 B): vertex normals, uvs, material.
 struct __align__(16) DevShade {
     float4 a;  // n0.xyz n1.x
@@ -153,6 +164,7 @@ struct SceneView {
     const DevNodeQ* nodesq;  // compressed 4-wide tree (RTG_QNODE)
     const float4* leafbox;   // [2 per triangle] exact box of the reference leaf holding it
     const DevTri* tris;
+    const DevTri48* tris48;  // same triangles, compact record (RTG_TRI48)
     const DevShade* shade;
     const DevMat* mats;
     const DevLight* lights;
@@ -352,6 +364,32 @@ RTG_D bool tri_intersect(const DevTri& T, v3 o, v3 d, float& t, float& u, float&
     float uu = dot(cross(e1, sub(p, v1)), n) * inv_area;
     if (uu < 0 || uu > 1.0f) return false;
     float vv = dot(cross(e2, sub(p, v2)), n) * inv_area;
+    if (vv < 0 || (uu + vv) > 1.0f) return false;
+    t = tt;
+    u = uu;
+    v = vv;
+    return true;
+}
+
+// Triangle::rayIntersect on the 48-B record. `want(t)` rejects a plane distance that cannot be a
+// candidate for the caller (beyond the current hit or not in front): those never produce output,
+// so the rest of the test (edge functions, 1/area) is skipped for them.
+template <typename W>
+RTG_D bool tri_intersect48(const DevTri48& T, v3 o, v3 d, W want, float& t, float& u, float& v) {
+    const v3 n = mk(T.a.x, T.a.y, T.a.z);
+    const float denom = dot(n, d);
+    if (denom == 0) return false;
+    const v3 v0 = mk(T.a.w, T.b.x, T.b.y);
+    const float dd = dot(n, v0);
+    const float tt = (dd - dot(n, o)) / denom;
+    if (tt < 0 || !want(tt)) return false;
+    const v3 v1 = mk(T.b.z, T.b.w, T.c.x), v2 = mk(T.c.y, T.c.z, T.c.w);
+    const v3 p = add(o, muls(d, tt));
+    const v3 e1 = sub(v2, v1), e2 = sub(v0, v2);
+    const float inv_area = 1.0f / dot(cross(e1, e2), n);
+    const float uu = dot(cross(e1, sub(p, v1)), n) * inv_area;
+    if (uu < 0 || uu > 1.0f) return false;
+    const float vv = dot(cross(e2, sub(p, v2)), n) * inv_area;
     if (vv < 0 || (uu + vv) > 1.0f) return false;
     t = tt;
     u = uu;

@@ -215,9 +215,17 @@ void k_trace(SceneView s, TraceIO io) {
             for (int k = 0; k < cnt; ++k) {
                 const int tri = start + k;
                 if (COUNT) (anyr ? c_stris : c_tris) += 1;
-                const DevTri T = s.tris[tri];
                 float t, u, v;
-                if (tri_intersect(T, o, d, t, u, v)) {
+#if RTG_TRI48
+                const DevTri48 T = s.tris48[tri];
+                const bool hit = tri_intersect48(T, o, d, [&](float tt) {
+                    return anyr ? (tt < tbest && tt > RTG_EPS) : (tt <= tbest && tt > RTG_EPS);
+                }, t, u, v);
+#else
+                const DevTri T = s.tris[tri];
+                const bool hit = tri_intersect(T, o, d, t, u, v);
+#endif
+                if (hit) {
                     bool cand = anyr ? !(t >= tbest || t <= RTG_EPS)
                                      : (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid)));
 #if RTG_QNODE
@@ -768,6 +776,7 @@ struct rtg_handle {
     int integrator = RTG_INTEGRATOR_PATH;
     uint32_t wide_depth = 0;  // wide levels on the longest root-to-leaf path
     DevTri* d_tris = nullptr;
+    DevTri48* d_tris48 = nullptr;
     DevShade* d_shade = nullptr;
     DevMat* d_mats = nullptr;
     DevLight* d_lights = nullptr;
@@ -928,6 +937,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
 
     // ---- triangles: Triangle::init (Geometry.h:72-83) + gNormal (:127-130)
     std::vector<DevTri> tris(nt);
+    std::vector<DevTri48> tris48(nt);
     std::vector<DevShade> shade(nt);
     std::vector<float> tri_area(nt), tri_gn(nt * 3);
     for (uint32_t i = 0; i < nt; ++i) {
@@ -949,6 +959,9 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         tris[i].v1i = make_float4(v1[0], v1[1], v1[2], inv_area);
         tris[i].v2 = make_float4(v2[0], v2[1], v2[2], 0.0f);
         tris[i].e2 = make_float4(e2[0], e2[1], e2[2], 0.0f);
+        tris48[i].a = make_float4(n[0], n[1], n[2], v0[0]);
+        tris48[i].b = make_float4(v0[1], v0[2], v1[0], v1[1]);
+        tris48[i].c = make_float4(v1[2], v2[0], v2[1], v2[2]);
         const float* U = d->uvs + (size_t)i * 6;
         if (d->material[i] >= d->n_materials) { g_err = "triangle material index out of range"; return RTG_ERR_ARG; }
         shade[i].a = make_float4(N[0], N[1], N[2], N[3]);
@@ -1152,7 +1165,11 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     if ((rc = dev_upload(&h->d_nodesw, nodesw))) return rc;
     if ((rc = dev_upload(&h->d_nodesq, nodesq))) return rc;
     if ((rc = dev_upload(&h->d_leafbox, leafbox))) return rc;
-    if ((rc = dev_upload(&h->d_tris, tris))) return rc;
+    if (RTG_TRI48) {
+        if ((rc = dev_upload(&h->d_tris48, tris48))) return rc;
+    } else if ((rc = dev_upload(&h->d_tris, tris))) {
+        return rc;
+    }
     if ((rc = dev_upload(&h->d_shade, shade))) return rc;
     if ((rc = dev_upload(&h->d_mats, mats))) return rc;
     if ((rc = dev_upload(&h->d_lights, lights))) return rc;
@@ -1162,6 +1179,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     SceneView& s = h->sv;
     s.nodes = h->d_nodes;
     s.tris = h->d_tris;
+    s.tris48 = h->d_tris48;
     s.shade = h->d_shade;
     s.mats = h->d_mats;
     s.lights = h->d_lights;
@@ -1224,7 +1242,7 @@ void rtg_destroy(rtg_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_chunk(h);
-    (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodesw); (void)hipFree(h->d_nodesq); (void)hipFree(h->d_leafbox); (void)hipFree(h->d_tris); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
+    (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodesw); (void)hipFree(h->d_nodesq); (void)hipFree(h->d_leafbox); (void)hipFree(h->d_tris); (void)hipFree(h->d_tris48); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
     (void)hipFree(h->d_lights); (void)hipFree(h->d_texinfo); (void)hipFree(h->d_texels); (void)hipFree(h->d_film);
     (void)hipFree(h->d_pix); (void)hipFree(h->d_ovf); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
     for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
