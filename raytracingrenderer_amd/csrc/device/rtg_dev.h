@@ -106,9 +106,20 @@ struct __align__(16) DevNodeW {
 #ifndef RTG_QNODE
 #define RTG_QNODE 1
 #endif
+// RTG_NODE48: the same node in 48 B (three dwordx4 loads). The origin keeps a 16-bit mantissa
+// (rounded down) and its low byte carries the axis exponent; the child words are 24-bit
+// (bit 23: leaf, 0xffffff: empty):
+//   q[0] = origin.x|exp.x, origin.y|exp.y, origin.z|exp.z, plane min x
+//   q[1] = planes min y, min z, max x, max y;   q[2] = plane max z, words (4 x 24 bits)
+#ifndef RTG_NODE48
+#define RTG_NODE48 0
+#endif
 struct __align__(16) DevNodeQ {
-    float4 q[4];
+    float4 q[RTG_NODE48 ? 3 : 4];
 };
+RTG_D int word24(unsigned w) {
+    return w == 0xffffffu ? RTG_EXIT : ((w & 0x800000u) ? ~(int)(w & 0x7fffffu) : (int)w);
+}
 typedef float f2 __attribute__((ext_vector_type(2)));  // packed FP32 pair (v_pk_fma/mul/add_f32)
 __host__ __device__ inline float qdecode(float origin, unsigned plane, int k, float scale) {
     return origin + (float)((plane >> (8 * k)) & 255u) * scale;
@@ -126,10 +137,16 @@ struct __align__(16) DevTri {
 #ifndef RTG_TRI48
 #define RTG_TRI48 1
 #endif
+#ifndef RTG_TRI_PAD
+#define RTG_TRI_PAD 0       // 1: 64-B stride (records never straddle a cache line), still 3 loads
+#endif
 struct __align__(16) DevTri48 {
     float4 a;  // n.xyz, v0.x
     float4 b;  // v0.yz, v1.xy
     float4 c;  // v1.z, v2.xyz
+#if RTG_TRI_PAD
+    float4 pad;
+#endif
 };
 // Cold shading record (64 B): vertex normals, uvs, material.
 struct __align__(16) DevShade {

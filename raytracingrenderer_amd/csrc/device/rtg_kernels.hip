@@ -258,6 +258,22 @@ void k_trace(SceneView s, TraceIO io) {
 #if RTG_QNODE
             {
                 const float4* np = s.nodesq[cur].q;
+#if RTG_NODE48
+                const float4 g0 = np[0], g1 = np[1], g2 = np[2];
+                const unsigned bx = __float_as_uint(g0.x), by = __float_as_uint(g0.y), bz = __float_as_uint(g0.z);
+                const float4 h0 = make_float4(__uint_as_float(bx & ~255u), __uint_as_float(by & ~255u),
+                                              __uint_as_float(bz & ~255u), 0.0f);
+                const float sx = __uint_as_float((bx & 255u) << 23);
+                const float sy = __uint_as_float((by & 255u) << 23);
+                const float sz = __uint_as_float((bz & 255u) << 23);
+                const unsigned p0 = __float_as_uint(g0.w), p1 = __float_as_uint(g1.x), p2 = __float_as_uint(g1.y);
+                const unsigned p3 = __float_as_uint(g1.z), p4 = __float_as_uint(g1.w), p5 = __float_as_uint(g2.x);
+                const unsigned w01 = __float_as_uint(g2.y), w12 = __float_as_uint(g2.z), w23 = __float_as_uint(g2.w);
+                wd[0] = word24(w01 & 0xffffffu);
+                wd[1] = word24((w01 >> 24) | ((w12 & 0xffffu) << 8));
+                wd[2] = word24((w12 >> 16) | ((w23 & 0xffu) << 16));
+                wd[3] = word24(w23 >> 8);
+#else
                 const float4 h0 = np[0], h1 = np[1], h2 = np[2], h3 = np[3];
                 const unsigned ex = __float_as_uint(h0.w);
                 const float sx = __uint_as_float((ex & 255u) << 23);
@@ -269,6 +285,7 @@ void k_trace(SceneView s, TraceIO io) {
                 wd[1] = __float_as_int(h2.w);
                 wd[2] = __float_as_int(h3.x);
                 wd[3] = __float_as_int(h3.y);
+#endif
                 // Conservative slot test in ray-relative form. Exactness does not need the exact slab
                 // test here: a candidate hit is accepted only after its reference leaf box passes the
                 // exact test, so a slot test only has to pass whenever the exact test on a reference
@@ -861,6 +878,14 @@ static bool encode_qnode(const float* bounds, const std::vector<int>& slots, con
             lo[a] = std::min(lo[a], bounds[(size_t)slots[k] * 6 + a]);
             hi[a] = std::max(hi[a], bounds[(size_t)slots[k] * 6 + 3 + a]);
         }
+        if (RTG_NODE48) {  // origin rounded down to a 16-bit mantissa (its low byte holds the exponent)
+            uint32_t b;
+            std::memcpy(&b, &lo[a], 4);
+            if ((int32_t)b >= 0) b &= ~0xffu;
+            else b = (b + 0xffu) & ~0xffu;
+            std::memcpy(&lo[a], &b, 4);
+            if (!std::isfinite(lo[a])) return false;
+        }
     }
     unsigned planes[6] = {0, 0, 0, 0, 0, 0};
     unsigned bexp[3];
@@ -889,10 +914,30 @@ static bool encode_qnode(const float* bounds, const std::vector<int>& slots, con
         }
     }
     auto uf = [](unsigned v) { float f; std::memcpy(&f, &v, 4); return f; };
+#if RTG_NODE48
+    unsigned w24[4];
+    for (int k = 0; k < 4; ++k) {
+        const int w = words[k];
+        if (w == RTG_EXIT) w24[k] = 0xffffffu;
+        else if (w < 0) {
+            if ((unsigned)~w >= 0x7fffffu) return false;  // leaf code must fit 23 bits
+            w24[k] = (unsigned)~w | 0x800000u;
+        } else {
+            if ((unsigned)w >= 0x800000u) return false;   // node index must fit 23 bits
+            w24[k] = (unsigned)w;
+        }
+    }
+    auto ob = [&](int a) { uint32_t b; std::memcpy(&b, &lo[a], 4); return b | bexp[a]; };
+    out.q[0] = make_float4(uf(ob(0)), uf(ob(1)), uf(ob(2)), uf(planes[0]));
+    out.q[1] = make_float4(uf(planes[1]), uf(planes[2]), uf(planes[3]), uf(planes[4]));
+    out.q[2] = make_float4(uf(planes[5]), uf(w24[0] | (w24[1] << 24)), uf((w24[1] >> 8) | (w24[2] << 16)),
+                           uf((w24[2] >> 16) | (w24[3] << 8)));
+#else
     out.q[0] = make_float4(lo[0], lo[1], lo[2], uf(bexp[0] | (bexp[1] << 8) | (bexp[2] << 16)));
     out.q[1] = make_float4(uf(planes[0]), uf(planes[1]), uf(planes[2]), uf(planes[3]));
     out.q[2] = make_float4(uf(planes[4]), uf(planes[5]), host_bits_f(words[0]), host_bits_f(words[1]));
     out.q[3] = make_float4(host_bits_f(words[2]), host_bits_f(words[3]), 0.0f, 0.0f);
+#endif
     return true;
 }
 static float host_dot(const float* a, const float* b) { return ((a[0] * b[0]) + (a[1] * b[1])) + (a[2] * b[2]); }
