@@ -70,6 +70,8 @@ void rth_free(void* p);
 /* C3 synthetic scene: n_tris random triangles, splitmix64 stream from seed,
  * written as .gem + scene.json + albedo .png + constant env.hdr so rth_load_scene loads it. */
 int  rth_write_synthetic(const char* dir, uint32_t n_tris, uint64_t seed, int32_t width, int32_t height);
+/* The same scene recipe around caller-given triangles (positions: 9 floats per triangle, face normals). */
+int  rth_write_mesh_scene(const char* dir, const float* positions, uint32_t n_tris, int32_t width, int32_t height);
 
 #ifdef __cplusplus
 }

@@ -95,6 +95,7 @@ RTH_EXPORTS = [
     ("rth_write_hdr", C.c_int, [C.c_char_p, C.c_int32, C.c_int32, f32p]),
     ("rth_read_hdr", C.c_int, [C.c_char_p, i32p, i32p, C.POINTER(f32p)]),
     ("rth_read_png", C.c_int, [C.c_char_p, i32p, i32p, i32p, C.POINTER(C.POINTER(C.c_uint8))]),
+    ("rth_write_mesh_scene", C.c_int, [C.c_char_p, f32p, C.c_uint32, C.c_int32, C.c_int32]),
     ("rth_read_ldr", C.c_int, [C.c_char_p, i32p, i32p, i32p, C.POINTER(C.POINTER(C.c_uint8))]),
     ("rth_tonemap", C.c_int, [C.c_int32, C.c_int32, f32p, C.c_uint32, C.c_float, C.POINTER(C.c_uint8)]),
     ("rth_save_png", C.c_int, [C.c_char_p, C.c_int32, C.c_int32, f32p, C.c_uint32]),

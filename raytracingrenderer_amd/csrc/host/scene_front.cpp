@@ -456,6 +456,28 @@ struct SplitMix {
 
 using namespace rth;
 
+// The C3 scene recipe around a mesh: diffuse albedo (185,181,173) PNG, constant
+// env.hdr 64x32 = 1.0 (lights[0]), camera at (0,0,3.5) looking at the origin, fov 45.
+static int write_mesh_scene(const std::string& d, const std::vector<GemVertex>& verts,
+                            const std::vector<uint32_t>& idx, int32_t width, int32_t height) {
+    if (!write_gem(d + "/synth.gem", verts, idx, g_err)) return RTG_ERR_ARG;
+    const uint8_t albedo[3] = {185, 181, 173};  // 0.725 0.71 0.68 (cornell white)
+    if (!encode_png(d + "/albedo.png", 1, 1, 3, albedo, g_err)) return RTG_ERR_ARG;
+    std::vector<float> env(64 * 32 * 3, 1.0f);
+    if (!encode_hdr(d + "/env.hdr", 64, 32, env.data(), g_err)) return RTG_ERR_ARG;
+    FILE* f = std::fopen((d + "/scene.json").c_str(), "w");
+    if (!f) { g_err = "cannot write scene.json"; return RTG_ERR_ARG; }
+    std::fprintf(f,
+                 "{\n    \"width\": \"%d\",\n    \"height\": \"%d\",\n    \"fov\": \"45.0\",\n"
+                 "    \"from\": \"0.0 0.0 3.5\",\n    \"to\": \"0.0 0.0 0.0\",\n    \"up\": \"0.0 1.0 0.0\",\n"
+                 "    \"envmap\": \"env.hdr\",\n    \"instances\": [{\n    \"filename\": \"synth.gem\",\n"
+                 "    \"world\": [1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0],\n"
+                 "    \"bsdf\": \"diffuse\",\n    \"reflectance\": \"albedo.png\"\n}]\n}\n",
+                 width, height);
+    std::fclose(f);
+    return RTG_OK;
+}
+
 extern "C" {
 
 const char* rth_last_error(void) { return g_err.c_str(); }
@@ -576,22 +598,28 @@ int rth_write_synthetic(const char* dir, uint32_t n_tris, uint64_t seed, int32_t
             idx[(size_t)t * 3 + k] = t * 3 + k;
         }
     }
-    if (!write_gem(d + "/synth.gem", verts, idx, g_err)) return RTG_ERR_ARG;
-    const uint8_t albedo[3] = {185, 181, 173};  // 0.725 0.71 0.68 (cornell white)
-    if (!encode_png(d + "/albedo.png", 1, 1, 3, albedo, g_err)) return RTG_ERR_ARG;
-    std::vector<float> env(64 * 32 * 3, 1.0f);
-    if (!encode_hdr(d + "/env.hdr", 64, 32, env.data(), g_err)) return RTG_ERR_ARG;
-    FILE* f = std::fopen((d + "/scene.json").c_str(), "w");
-    if (!f) { g_err = "cannot write scene.json"; return RTG_ERR_ARG; }
-    std::fprintf(f,
-                 "{\n    \"width\": \"%d\",\n    \"height\": \"%d\",\n    \"fov\": \"45.0\",\n"
-                 "    \"from\": \"0.0 0.0 3.5\",\n    \"to\": \"0.0 0.0 0.0\",\n    \"up\": \"0.0 1.0 0.0\",\n"
-                 "    \"envmap\": \"env.hdr\",\n    \"instances\": [{\n    \"filename\": \"synth.gem\",\n"
-                 "    \"world\": [1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, 1.0],\n"
-                 "    \"bsdf\": \"diffuse\",\n    \"reflectance\": \"albedo.png\"\n}]\n}\n",
-                 width, height);
-    std::fclose(f);
-    return RTG_OK;
+    return write_mesh_scene(d, verts, idx, width, height);
+}
+
+int rth_write_mesh_scene(const char* dir, const float* positions, uint32_t n_tris, int32_t width, int32_t height) {
+    if (!dir || (!positions && n_tris)) return RTG_ERR_ARG;
+    std::string d(dir);
+    ::mkdir(d.c_str(), 0755);
+    std::vector<GemVertex> verts((size_t)n_tris * 3);
+    std::vector<uint32_t> idx((size_t)n_tris * 3);
+    for (uint32_t t = 0; t < n_tris; ++t) {
+        const float* P = positions + (size_t)t * 9;
+        V3 p[3] = {V3(P[0], P[1], P[2]), V3(P[3], P[4], P[5]), V3(P[6], P[7], P[8])};
+        V3 n = (p[1] - p[0]).cross(p[2] - p[0]).normalize();
+        for (int k = 0; k < 3; ++k) {
+            GemVertex& g = verts[(size_t)t * 3 + k];
+            std::memset(&g, 0, sizeof(g));
+            g.pos[0] = p[k].x; g.pos[1] = p[k].y; g.pos[2] = p[k].z;
+            g.normal[0] = n.x; g.normal[1] = n.y; g.normal[2] = n.z;
+            idx[(size_t)t * 3 + k] = t * 3 + k;
+        }
+    }
+    return write_mesh_scene(d, verts, idx, width, height);
 }
 
 }  // extern "C"

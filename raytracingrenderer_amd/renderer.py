@@ -115,6 +115,16 @@ def write_synthetic_scene(out_dir, n_tris=1_000_000, seed=20251015, width=1024, 
     return out_dir
 
 
+def write_mesh_scene(out_dir, positions, width=256, height=256):
+    """The C3 scene recipe (diffuse albedo, constant env light, fixed camera) around caller-given
+    triangles: positions (n, 3, 3) float32."""
+    p = np.ascontiguousarray(positions, np.float32).reshape(-1, 9)
+    os.makedirs(out_dir, exist_ok=True)
+    _check(N.rth().rth_write_mesh_scene(os.fsencode(out_dir), N.ptr(p, C.c_float), len(p), width, height),
+           N.rth().rth_last_error)
+    return out_dir
+
+
 def save_hdr(path, film_sum, spp):
     """Film::save: film / SPP -> RLE RGBE (stbi_write_hdr format)."""
     f = np.ascontiguousarray(film_sum, np.float32)
