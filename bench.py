@@ -3,7 +3,7 @@
 vs peak" on config C3 (synthetic 1M random triangles, 1024x1024, 64 spp, MAX_DEPTH 4).
 
 One step = one complete 1024x1024x64spp render (64 RayTracer::render() frames) of this rank's
-32x32 tiles (tile_id % world_size == rank) through the HIP wavefront tracer, plus, for N > 1, the
+32x32 tiles ((tile_x + tile_y) % world_size == rank) through the HIP wavefront tracer, plus, for N > 1, the
 RCCL reduce(sum) of the float32 radiance film to rank 0 over xGMI (tile supports are disjoint, so
 the reduced film is bit-identical to a 1-GPU render). Total work is fixed as N grows (strong
 scaling). Scene generation, loading and BVH build happen before the timed region.
