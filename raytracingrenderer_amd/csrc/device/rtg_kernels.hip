@@ -44,6 +44,9 @@ using namespace rtgd;
 #ifndef RTG_POSTPONE
 #define RTG_POSTPONE 32     // >0: park a reached leaf and keep walking; run the leaves of a wave together
 #endif                      //     once this many lanes hold one (or no lane can walk on)
+#ifndef RTG_DRAIN_LEAF
+#define RTG_DRAIN_LEAF 1    // once the queue is empty, run the leaf phase whenever a lane has parked a
+#endif                      //     leaf (the drain is latency-bound: lanes should not wait for each other)
 #ifndef RTG_REFILL
 #define RTG_REFILL 16       // refill idle lanes once at least this many are idle (the setup code then
 #endif                      // runs with more lanes per execution)
@@ -79,6 +82,7 @@ struct TraceIO {
     unsigned long long* stats; // [0,1] closest / [4,5] any-hit: box tests, triangle tests (COUNT)
     int cull;
     int wide;                  // traverse the 4-wide tree when the ray allows it
+    unsigned long long* wtime; // diagnostics (RTG_WAVETIME): per wave start / drained / exit clock
 };
 
 struct ChunkArgs {
@@ -138,6 +142,8 @@ void k_trace(SceneView s, TraceIO io) {
     float tbest = 0.0f, omag = 0.0f, dmag = 0.0f, delta = 0.0f, bu = 0.0f, bv = 0.0f;
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0, pend = RTG_EXIT;
     bool occluded = false, wide = false, anyr = false;  // anyr: this lane's ray is a shadow ray
+    const unsigned wslot = gtid >> 6;
+    if (io.wtime && lane == 0) io.wtime[3 * wslot] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         // ---- retire finished rays
         if (have && cur == RTG_EXIT && pend == RTG_EXIT) {
@@ -158,6 +164,7 @@ void k_trace(SceneView s, TraceIO io) {
                 b = __shfl(b, 0);
                 if (b >= n) {
                     drained = true;
+                    if (io.wtime && lane == 0) io.wtime[3 * wslot + 1] = __builtin_amdgcn_s_memrealtime();
                 } else {
                     pool_base = b;
                     pool_left = min(64u, n - b);
@@ -456,7 +463,7 @@ void k_trace(SceneView s, TraceIO io) {
 #if RTG_POSTPONE
         // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on
         const unsigned long long pm = __ballot(pend != RTG_EXIT);
-        if (__popcll(pm) >= RTG_POSTPONE || __ballot(cur >= 0) == 0) {
+        if (__popcll(pm) >= RTG_POSTPONE || __ballot(cur >= 0) == 0 || (RTG_DRAIN_LEAF && drained && pm)) {
             if (COUNT) {
                 c_lslots += 64;
                 c_lstep += pend != RTG_EXIT ? 1 : 0;
@@ -472,6 +479,7 @@ void k_trace(SceneView s, TraceIO io) {
         }
 #endif
     }
+    if (io.wtime && lane == 0) io.wtime[3 * wslot + 2] = __builtin_amdgcn_s_memrealtime();
     if (COUNT) {
         for (int off = 32; off > 0; off >>= 1) {
             c_nodes += __shfl_down(c_nodes, off);
@@ -749,8 +757,8 @@ __global__ void k_tally(const Counters* ctr, int maxb, unsigned long long* stats
         e += ctr[b].n_ext;
         sh += ctr[b].n_shadow;
     }
-    stats[2] += e;
-    stats[3] += sh;
+    atomicAdd(&stats[2], e);  // chunk pipelines may tally concurrently
+    atomicAdd(&stats[3], sh);
 }
 
 // ================================================================== host side (C-ABI)
@@ -801,9 +809,13 @@ struct rtg_handle {
     float* d_texels = nullptr;
     float* d_film = nullptr;
     // chunk buffers
-    size_t cap_P = 0;
-    int cap_maxb = 0;
-    PathBufs pb{};
+    // two chunk pipelines (buffers, stream, overflow region each): pipeline 1 runs on stream2
+    size_t cap_P[2] = {0, 0};
+    int cap_maxb[2] = {0, 0};
+    PathBufs pb[2]{};
+    hipStream_t stream2 = nullptr;
+    int pipes = 1, stagger = 2;
+    hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};  // fork, stagger, join, accumulate-order
     unsigned* d_pix = nullptr;
     size_t cap_pix = 0;
     std::vector<uint32_t> pix_key;
@@ -817,20 +829,21 @@ struct rtg_handle {
     std::vector<hipEvent_t> kev;  // per-launch timing events (timing mode)
 };
 
-static void free_chunk(rtg_handle* h) {
-    (void)hipFree(h->pb.thr); (void)hipFree(h->pb.rng); (void)hipFree(h->pb.meta); (void)hipFree(h->pb.contrib);
-    (void)hipFree(h->pb.q[0]); (void)hipFree(h->pb.q[1]); (void)hipFree(h->pb.hits); (void)hipFree(h->pb.shq); (void)hipFree(h->pb.ctr);
-    (void)hipFree(h->pb.ray_o); (void)hipFree(h->pb.ray_d);
-    (void)hipFree(h->pb.sh_o); (void)hipFree(h->pb.sh_d); (void)hipFree(h->pb.sh_c);
-    h->pb = PathBufs{};
-    h->cap_P = 0;
-    h->cap_maxb = 0;
+static void free_chunk(rtg_handle* h, int i) {
+    PathBufs& p = h->pb[i];
+    (void)hipFree(p.thr); (void)hipFree(p.rng); (void)hipFree(p.meta); (void)hipFree(p.contrib);
+    (void)hipFree(p.q[0]); (void)hipFree(p.q[1]); (void)hipFree(p.hits); (void)hipFree(p.shq); (void)hipFree(p.ctr);
+    (void)hipFree(p.ray_o); (void)hipFree(p.ray_d);
+    (void)hipFree(p.sh_o); (void)hipFree(p.sh_d); (void)hipFree(p.sh_c);
+    p = PathBufs{};
+    h->cap_P[i] = 0;
+    h->cap_maxb[i] = 0;
 }
 
-static int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
-    if (P <= h->cap_P && maxb <= h->cap_maxb) return RTG_OK;
-    free_chunk(h);
-    PathBufs& p = h->pb;
+static int ensure_chunk(rtg_handle* h, int i, size_t P, int maxb) {
+    if (P <= h->cap_P[i] && maxb <= h->cap_maxb[i]) return RTG_OK;
+    free_chunk(h, i);
+    PathBufs& p = h->pb[i];
     HIPOK(hipMalloc((void**)&p.thr, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.rng, P * sizeof(unsigned long long)));
     HIPOK(hipMalloc((void**)&p.meta, P * sizeof(int)));
@@ -845,8 +858,8 @@ static int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
     HIPOK(hipMalloc((void**)&p.sh_d, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.sh_c, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.ctr, (size_t)(maxb + 1) * sizeof(Counters)));
-    h->cap_P = P;
-    h->cap_maxb = maxb;
+    h->cap_P[i] = P;
+    h->cap_maxb[i] = maxb;
     return RTG_OK;
 }
 
@@ -856,7 +869,7 @@ static int ensure_ovf(rtg_handle* h) {
     // level descends at least one BVH2 level)
     size_t deep = std::max<size_t>(h->bvh_depth, (size_t)h->wide_depth * (RTG_WIDTH - 1)) + 2;
     size_t levels = deep > RTG_STACK ? deep - RTG_STACK : 1;
-    size_t need = levels * (size_t)grid * RTG_TB;
+    size_t need = 2 * levels * (size_t)grid * RTG_TB;  // one region per chunk pipeline
     if (need <= h->cap_ovf) return RTG_OK;
     (void)hipFree(h->d_ovf);
     HIPOK(hipMalloc((void**)&h->d_ovf, need * sizeof(int)));
@@ -1257,6 +1270,10 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     HIPOK(hipMalloc((void**)&h->d_stats, 16 * sizeof(unsigned long long)));
     HIPOK(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
     for (auto& e : h->ev) HIPOK(hipEventCreate(&e));
+    for (auto& e : h->pev) HIPOK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPOK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
+    if (const char* e = std::getenv("RTG_PIPES")) h->pipes = std::atoi(e) >= 2 ? 2 : 1;
+    if (const char* e = std::getenv("RTG_STAGGER")) h->stagger = std::atoi(e);
 
     int occ = 0;
     HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false>, RTG_TB, 0));
@@ -1286,13 +1303,17 @@ void rtg_destroy(rtg_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    free_chunk(h);
+    if (h->stream2) (void)hipStreamSynchronize(h->stream2);
+    free_chunk(h, 0);
+    free_chunk(h, 1);
     (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodesw); (void)hipFree(h->d_nodesq); (void)hipFree(h->d_leafbox); (void)hipFree(h->d_tris); (void)hipFree(h->d_tris48); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
     (void)hipFree(h->d_lights); (void)hipFree(h->d_texinfo); (void)hipFree(h->d_texels); (void)hipFree(h->d_film);
     (void)hipFree(h->d_pix); (void)hipFree(h->d_ovf); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
     for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
+    for (auto& e : h->pev) if (e) (void)hipEventDestroy(e);
     for (auto& e : h->kev) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
+    if (h->stream2) (void)hipStreamDestroy(h->stream2);
     delete h;
 }
 
@@ -1375,19 +1396,45 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
     if ((uint64_t)first + n_samples > 65536u) { g_err = "sample index >= 65536 (PCG stream key)"; return RTG_ERR_ARG; }
     const int maxb = h->max_depth + 2;
     uint32_t ns_chunk = std::max<uint32_t>(1, std::min<uint32_t>(n_samples, h->max_paths / std::max(1u, h->npix)));
+    // Two chunk pipelines: the samples are split into (at least) two chunks that alternate between
+    // the caller's stream and stream2, so that one chunk's trace drain tails (a few hundred us per
+    // launch: the longest rays' dependent fetch chains) overlap the other chunk's work. The film
+    // fold stays in sample order: chunk c's k_accumulate waits for chunk c-1's.
+    const int pipes = (h->pipes >= 2 && n_samples >= 2) ? 2 : 1;
+    if (pipes == 2 && ns_chunk >= n_samples) ns_chunk = (n_samples + 1) / 2;
     const size_t P = (size_t)ns_chunk * h->npix;
-    if ((rc = ensure_chunk(h, P, maxb))) return rc;
+    for (int i = 0; i < pipes; ++i)
+        if ((rc = ensure_chunk(h, i, P, maxb))) return rc;
     if ((rc = ensure_ovf(h))) return rc;
     (void)hipGetLastError();  // drop any stale error left by other code on this thread
     HIPOK(hipEventRecord(h->ev[0], st));
+    if (pipes == 2) {  // stream2 starts after everything already queued on the caller's stream
+        HIPOK(hipEventRecord(h->pev[0], st));
+        HIPOK(hipStreamWaitEvent(h->stream2, h->pev[0], 0));
+    }
     std::vector<int> kinds;  // 0 extend, 1 shadow, 2 other (timing mode)
     size_t k = 0;
     TraceIO io{};
-    io.ovf = h->d_ovf;
     io.stats = h->d_stats;
     io.cull = h->cull;
     io.wide = h->wide;
-    for (uint32_t s0 = first; s0 < first + n_samples; s0 += ns_chunk) {
+    // RTG_WAVETIME (diagnostic): per-wave clocks of chunk 0's trace launches, summarised on stderr
+    unsigned long long* d_wt = nullptr;
+    const size_t wt_waves = (size_t)std::max(h->trace_blocks, h->trace_blocks_count) * (RTG_TB / 64);
+    if (std::getenv("RTG_WAVETIME")) {
+        HIPOK(hipMalloc((void**)&d_wt, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long)));
+        HIPOK(hipMemsetAsync(d_wt, 0, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long), st));
+    }
+    uint32_t c = 0;
+    for (uint32_t s0 = first; s0 < first + n_samples; s0 += ns_chunk, ++c) {
+        const int pi = pipes == 2 ? (int)(c & 1) : 0;
+        hipStream_t cs = pi ? h->stream2 : st;
+        PathBufs& pb = h->pb[pi];
+        io.ovf = h->d_ovf + (size_t)pi * (h->cap_ovf / 2);
+        // stagger: chunk 1 starts after chunk 0's generate (1) or first trace launch (2), so the
+        // two pipelines' drain tails fall at different times (0: both start together)
+        if (pipes == 2 && c == 1 && (h->stagger == 1 || h->stagger == 2))
+            HIPOK(hipStreamWaitEvent(cs, h->pev[1], 0));
         ChunkArgs a;
         a.pixlist = h->d_pix;
         a.npix = h->npix;
@@ -1398,46 +1445,84 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
         a.max_depth = h->max_depth;
         a.mode = h->integrator;
         a.cam = h->cam;
-        HIPOK(hipMemsetAsync(h->pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), st));
-        timed_begin(h, st, k);
-        hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, h->pb);
+        HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), cs));
+        timed_begin(h, cs, k);
+        hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, cs, a, pb);
         LAUNCH_OK("k_generate");
-        timed_end(h, st, k); kinds.push_back(2); ++k;
+        timed_end(h, cs, k); kinds.push_back(2); ++k;
+        if (pipes == 2 && c == 0 && h->stagger == 1) HIPOK(hipEventRecord(h->pev[1], cs));
         // Trace launch L_b (b = 0..maxb) carries the extension rays of bounce b (from shade(b-1),
         // or generate) and the shadow rays of bounce b-1: one persistent launch, one drain tail.
         for (int b = 0; b <= maxb; ++b) {
             if (b > 0) {
-                timed_begin(h, st, k);
-                hipLaunchKernelGGL(k_shade, dim3(h->shade_blocks), dim3(RTG_TB), 0, st, h->sv, a, h->pb, b - 1);
+                timed_begin(h, cs, k);
+                hipLaunchKernelGGL(k_shade, dim3(h->shade_blocks), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
                 LAUNCH_OK("k_shade");
-                timed_end(h, st, k); kinds.push_back(2); ++k;
+                timed_end(h, cs, k); kinds.push_back(2); ++k;
             }
-            io.queue = h->pb.q[b & 1];
-            io.ray_o = h->pb.ray_o;
-            io.ray_d = h->pb.ray_d;
-            io.count = b < maxb ? &h->pb.ctr[b].n_ext : nullptr;
-            io.hits = h->pb.hits;
-            io.squeue = h->pb.shq;
-            io.sray_o = h->pb.sh_o;
-            io.sray_d = h->pb.sh_d;
-            io.sray_c = h->pb.sh_c;
-            io.scount = b > 0 ? &h->pb.ctr[b - 1].n_shadow : nullptr;
-            io.contrib = b > 0 ? h->pb.contrib + (size_t)(b - 1) * a.P : nullptr;
+            io.queue = pb.q[b & 1];
+            io.ray_o = pb.ray_o;
+            io.ray_d = pb.ray_d;
+            io.count = b < maxb ? &pb.ctr[b].n_ext : nullptr;
+            io.hits = pb.hits;
+            io.squeue = pb.shq;
+            io.sray_o = pb.sh_o;
+            io.sray_d = pb.sh_d;
+            io.sray_c = pb.sh_c;
+            io.scount = b > 0 ? &pb.ctr[b - 1].n_shadow : nullptr;
+            io.contrib = b > 0 ? pb.contrib + (size_t)(b - 1) * a.P : nullptr;
             io.visible = nullptr;
-            io.fetch = &h->pb.ctr[b].f_ext;
-            timed_begin(h, st, k);
-            if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
-            else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
+            io.fetch = &pb.ctr[b].f_ext;
+            io.wtime = (d_wt && c == 0) ? d_wt + (size_t)b * wt_waves * 3 : nullptr;
+            timed_begin(h, cs, k);
+            if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, cs, h->sv, io);
+            else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, cs, h->sv, io);
             LAUNCH_OK("k_trace");
-            timed_end(h, st, k); kinds.push_back(0); ++k;
+            timed_end(h, cs, k); kinds.push_back(0); ++k;
+            if (pipes == 2 && c == 0 && b == 0 && h->stagger == 2) HIPOK(hipEventRecord(h->pev[1], cs));
         }
-        hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, st, h->pb.ctr, maxb, h->d_stats);
+        hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, cs, pb.ctr, maxb, h->d_stats);
         LAUNCH_OK("k_tally");
-        timed_begin(h, st, k);
-        hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, h->pb, h->d_film);
+        if (pipes == 2 && c > 0) HIPOK(hipStreamWaitEvent(cs, h->pev[3], 0));  // fold order
+        timed_begin(h, cs, k);
+        hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, cs, a, pb, h->d_film);
         LAUNCH_OK("k_accumulate");
-        timed_end(h, st, k); kinds.push_back(2); ++k;
+        timed_end(h, cs, k); kinds.push_back(2); ++k;
+        if (pipes == 2) HIPOK(hipEventRecord(h->pev[3], cs));
         h->stats.paths += a.P;
+    }
+    if (pipes == 2) {  // join: the caller's stream waits for stream2's chunks
+        HIPOK(hipEventRecord(h->pev[2], h->stream2));
+        HIPOK(hipStreamWaitEvent(st, h->pev[2], 0));
+    }
+    if (d_wt) {
+        std::vector<unsigned long long> wt((size_t)(maxb + 1) * wt_waves * 3);
+        HIPOK(hipStreamSynchronize(st));
+        HIPOK(hipMemcpy(wt.data(), d_wt, wt.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        (void)hipFree(d_wt);
+        for (int b = 0; b <= maxb; ++b) {
+            const unsigned long long* w = wt.data() + (size_t)b * wt_waves * 3;
+            unsigned long long t0 = ~0ull, e0 = ~0ull;
+            std::vector<double> ends, starts;
+            for (size_t i = 0; i < wt_waves; ++i) {
+                if (!w[3 * i]) continue;
+                t0 = std::min(t0, w[3 * i]);
+                if (w[3 * i + 1]) e0 = std::min(e0, w[3 * i + 1]);
+            }
+            for (size_t i = 0; i < wt_waves; ++i) {
+                if (!w[3 * i]) continue;
+                starts.push_back((w[3 * i] - t0) * 0.01);  // 100 MHz clock -> us
+                ends.push_back((w[3 * i + 2] - t0) * 0.01);
+            }
+            if (ends.empty()) continue;
+            std::sort(ends.begin(), ends.end());
+            std::sort(starts.begin(), starts.end());
+            auto pct = [](const std::vector<double>& v, double q) { return v[std::min(v.size() - 1, (size_t)(q * v.size()))]; };
+            std::fprintf(stderr, "[wavetime] launch %d waves %zu start p50 %.1f max %.1f | queue empty %.1f | "
+                         "wave end p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f us\n", b, ends.size(), pct(starts, 0.5),
+                         starts.back(), (e0 - t0) * 0.01, pct(ends, 0.1), pct(ends, 0.5), pct(ends, 0.9), pct(ends, 0.99),
+                         ends.back());
+        }
     }
     HIPOK(hipEventRecord(h->ev[1], st));
     h->spp += n_samples;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# build A/B variants of librtg into raytracingrenderer_amd/lib/ab: mkab.sh name "-DFOO=1" [name "-D..."]...
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p raytracingrenderer_amd/lib/ab
+while [ $# -ge 2 ]; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -shared $2 \
+    -o raytracingrenderer_amd/lib/ab/$1.so raytracingrenderer_amd/csrc/device/rtg_kernels.hip &
+  shift 2
+done
+wait
