@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 1
+#define RTG_ABI_VERSION 2
 
 /* error codes */
 #define RTG_OK              0
@@ -54,6 +54,13 @@ typedef struct rtg_camera {        /* Camera, RTBase/Scene.h:10-70 */
     float origin[3];               /* origin = camera.mulPoint(0,0,0)         */
     float width, height;           /* film size as the reference floats       */
 } rtg_camera;
+
+typedef struct rtg_camera_proj {   /* Camera members used by projectOntoCamera / connectToCamera   */
+    float proj[16];                /* projectionMatrix.m (Scene.h:22-32, after the flipX negation)  */
+    float camera_to_view[16];      /* cameraToView.m = camera.invert() (Scene.h:33-41)             */
+    float view_direction[3];       /* viewDirection (Scene.h:38-40)                                */
+    float a_film;                  /* Afilm = Wlens * Hlens (Scene.h:28-31)                         */
+} rtg_camera_proj;
 
 typedef struct rtg_material {      /* BSDF* + emission, RTBase/Materials.h:94-116 */
     int32_t kind;                  /* RTG_MAT_*                                    */
@@ -85,6 +92,7 @@ typedef struct rtg_scene_desc {    /* Scene after Scene::build(), RTBase/Scene.h
     uint32_t n_lights;             /* Scene::lights in order                                   */
     const int32_t* lights;         /* -1 = the environment light, else a triangle index        */
     rtg_camera camera;
+    rtg_camera_proj projection;    /* light tracing / instant radiosity only (ABI version 2)   */
 } rtg_scene_desc;
 
 typedef struct rtg_stats {
@@ -136,11 +144,14 @@ int  rtg_set_options(rtg_handle* h, int max_depth, int flags, uint32_t max_paths
  * pathTrace (Renderer.h:328-392, the default). DIRECT = RayTracer::direct (:393-407): emission or one
  * NEE sample at the first hit, 0 on a miss. ALBEDO = RayTracer::albedo (:558-571): emission,
  * BSDF::evaluate(sd, (0,1,0)) or the background. NORMALS = RayTracer::viewNormals (:572-582):
- * |shading normal| at the first hit. */
-#define RTG_INTEGRATOR_PATH    0
-#define RTG_INTEGRATOR_DIRECT  1
-#define RTG_INTEGRATOR_ALBEDO  2
-#define RTG_INTEGRATOR_NORMALS 3
+ * |shading normal| at the first hit. DIRECT_MIS = RayTracer::direct with computeDirectMIS
+ * (:474-557) in place of computeDirect: one light sample and one BSDF sample combined by the
+ * balance heuristic (the reference defines it but never calls it). */
+#define RTG_INTEGRATOR_PATH       0
+#define RTG_INTEGRATOR_DIRECT     1
+#define RTG_INTEGRATOR_ALBEDO     2
+#define RTG_INTEGRATOR_NORMALS    3
+#define RTG_INTEGRATOR_DIRECT_MIS 4
 int  rtg_set_integrator(rtg_handle* h, int integrator);
 
 /* Add samples [first_sample, first_sample+n_samples) of every pixel in the listed 32x32 tiles
@@ -152,6 +163,34 @@ int  rtg_render(rtg_handle* h, uint32_t first_sample, uint32_t n_samples, uint64
 int  rtg_render_async(rtg_handle* h, uint32_t first_sample, uint32_t n_samples, uint64_t seed,
                       const uint32_t* tile_ids, uint32_t n_tiles, void* hip_stream);
 int  rtg_synchronize(rtg_handle* h);
+
+/* RayTracer::adaptiveRender (Renderer.h:583-749), one frame (Film::SPP += 1). Pass 1 renders
+ * init_samples samples of every pixel (sample indices first_sample ...) into a scratch film and
+ * takes each 32x32 tile's variance of the per-pixel means (adaptiveSampling, :583-638); a tile's
+ * weight is its share of the total variance; pass 2 renders max((int)(sqrt(weight) * max_samples),
+ * min_samples) samples of each pixel of the tile (indices first_sample + init_samples ...) and adds
+ * their mean to the film (sampleTileWithWeight, :640-672). The reference constants are INIT_SAMPLES
+ * 2, MAX_SAMPLES 10240, MIN_SAMPLES 1 (Renderer.h:20-23). tile_samples (optional, tilesX*tilesY)
+ * receives each tile's pass-2 sample count. */
+/* RayTracer::lightTracer (Renderer.h:221-326): each frame traces width*height light paths (path i
+ * of frame f draws from the PCG stream keyed (seed, i, f)), connects every non-specular vertex to
+ * the camera (connectToCamera: projectOntoCamera, importance W_e = 1/(Afilm cos^4), visibility)
+ * and splats the result into the film in (path, vertex) order per pixel, as the reference's
+ * single-threaded loop does. Film::SPP += 1 per frame. The film must have < 2^24 pixels. */
+int  rtg_render_light(rtg_handle* h, uint32_t first_frame, uint32_t n_frames, uint64_t seed);
+/* RayTracer::instantRadiosity (Renderer.h:82-218): each frame traces n_vpl_paths VPL paths
+ * (traceVPLs; the reference uses MAX_VPL = 50) and then, for every pixel whose camera ray hits a
+ * surface, sums vpl.Le * BSDF * G over every visible VPL in VPL order (computeVPLsContribution)
+ * and splats it. Film::SPP += 1 per frame. */
+#define RTG_MAX_VPL 50
+int  rtg_render_instant_radiosity(rtg_handle* h, uint32_t first_frame, uint32_t n_frames, uint64_t seed,
+                                  uint32_t n_vpl_paths);
+
+#define RTG_ADAPTIVE_INIT_SAMPLES 2
+#define RTG_ADAPTIVE_MAX_SAMPLES  10240
+#define RTG_ADAPTIVE_MIN_SAMPLES  1
+int  rtg_render_adaptive(rtg_handle* h, uint32_t first_sample, uint64_t seed, uint32_t init_samples,
+                         uint32_t max_samples, uint32_t min_samples, uint32_t* tile_samples);
 
 /* Film access: the unnormalised sum (Film::film) and the sample count (Film::SPP). */
 int  rtg_film_read(rtg_handle* h, float* rgb_sum /* width*height*3 */, uint32_t* spp);

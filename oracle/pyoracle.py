@@ -27,6 +27,14 @@ def lib(flavour="rtm"):
         L.or_render.restype = C.c_int
         L.or_render.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32, C.c_int, f32p,
                                 C.POINTER(C.c_uint64), C.c_int]
+        L.or_render_adaptive.restype = C.c_int
+        L.or_render_adaptive.argtypes = [vp, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, f32p, u32p]
+        L.or_render_light.restype = C.c_int
+        L.or_render_light.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint64, f32p]
+        L.or_render_ir.restype = C.c_int
+        L.or_render_ir.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, f32p]
+        L.or_camera_project.argtypes = [vp, f32p, C.c_uint32, f32p]
+        L.or_light_emit.argtypes = [vp, C.c_int, f32p, f32p]
         L.or_trace_paths.argtypes = [vp, u32p, u32p, C.c_uint32, C.c_uint64, f32p]
         L.or_trace_closest.argtypes = [vp, f32p, C.c_uint32, f32p]
         L.or_trace_visible.argtypes = [vp, f32p, C.c_uint32, i32p]
@@ -70,6 +78,44 @@ class Oracle:
         if rc != 0:
             raise RuntimeError("or_render failed")
         return film, counts
+
+    def render_adaptive(self, first=0, seed=1234, init=2, max_samples=10240, min_samples=1, film=None):
+        if film is None:
+            film = np.zeros((self.H, self.W, 3), np.float32)
+        nt = ((self.W + 31) // 32) * ((self.H + 31) // 32)
+        counts = np.zeros(nt, np.uint32)
+        rc = self.L.or_render_adaptive(self.h, first, seed, init, max_samples, min_samples, _p(film, C.c_float),
+                                       _p(counts, C.c_uint32))
+        if rc != 0:
+            raise RuntimeError("or_render_adaptive failed")
+        return film, counts
+
+    def render_light(self, n_frames=1, first=0, seed=1234, film=None):
+        if film is None:
+            film = np.zeros((self.H, self.W, 3), np.float32)
+        if self.L.or_render_light(self.h, first, n_frames, seed, _p(film, C.c_float)) != 0:
+            raise RuntimeError("or_render_light failed")
+        return film
+
+    def render_instant_radiosity(self, n_frames=1, first=0, seed=1234, n_vpl=50, film=None):
+        if film is None:
+            film = np.zeros((self.H, self.W, 3), np.float32)
+        if self.L.or_render_ir(self.h, first, n_frames, seed, n_vpl, _p(film, C.c_float)) != 0:
+            raise RuntimeError("or_render_ir failed")
+        return film
+
+    def camera_project(self, pts):
+        p = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
+        out = np.zeros((len(p), 3), np.float32)
+        self.L.or_camera_project(self.h, _p(p, C.c_float), len(p), _p(out, C.c_float))
+        return out
+
+    def light_emit(self, li, draws):
+        d = np.ascontiguousarray(draws, np.float32)
+        out = np.zeros(12, np.float32)
+        if self.L.or_light_emit(self.h, int(li), _p(d, C.c_float), _p(out, C.c_float)) != 0:
+            raise ValueError("not an area light")
+        return out
 
     def trace_paths(self, pixels, samples, seed=1234):
         p = np.ascontiguousarray(pixels, np.uint32)

@@ -24,7 +24,8 @@ def lib(flavour="libm"):
         L.ref_load.restype = vp
         L.ref_load.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_char_p]
         for name in ("ref_counts", "ref_export", "ref_texture_size", "ref_texture_texels", "ref_traverse",
-                     "ref_traverse_visible", "ref_visible", "ref_camera_rays", "ref_env_eval", "ref_tex_sample"):
+                     "ref_traverse_visible", "ref_visible", "ref_camera_rays", "ref_env_eval", "ref_tex_sample",
+                     "ref_camera_project", "ref_light_emit"):
             getattr(L, name).restype = None
         L.ref_bsdf_sample.restype = None
         L.ref_save_hdr.restype = C.c_int
@@ -38,8 +39,8 @@ def _p(a):
 
 
 class RefScene:
-    def __init__(self, scene_dir, width=0, height=0, skip_missing=False, envmap=None):
-        self.L = lib()
+    def __init__(self, scene_dir, width=0, height=0, skip_missing=False, envmap=None, flavour="libm"):
+        self.L = lib(flavour)
         self.h = self.L.ref_load(os.fsencode(scene_dir), width, height, 1 if skip_missing else 0,
                                  envmap.encode() if envmap else None)
         c = np.zeros(8, np.int32)
@@ -80,6 +81,19 @@ class RefScene:
         p = np.ascontiguousarray(pixels, np.uint32)
         out = np.zeros((len(p), 6), np.float32)
         self.L.ref_camera_rays(C.c_void_p(self.h), _p(p), len(p), _p(out))
+        return out
+
+    def camera_project(self, pts):
+        p = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
+        out = np.zeros((len(p), 3), np.float32)
+        state = np.zeros(36, np.float32)
+        self.L.ref_camera_project(C.c_void_p(self.h), _p(p), len(p), _p(out), _p(state))
+        return out, state
+
+    def light_emit(self, li, draws):
+        d = np.ascontiguousarray(draws, np.float32)
+        out = np.zeros(12, np.float32)
+        self.L.ref_light_emit(C.c_void_p(self.h), int(li), _p(d), len(d), _p(out))
         return out
 
     def env_eval(self, tex, dirs):

@@ -403,4 +403,36 @@ int ref_load_texture(const char* path, float* out, int cap, int* wh) {
     return n;
 }
 
+// Camera::projectOntoCamera (Scene.h:55-69) on points (xyz): out (ok, x, y) per point; state =
+// projectionMatrix[16], cameraToView[16], viewDirection[3], Afilm (the members light tracing uses).
+void ref_camera_project(void* h, const float* pts, int n, float* out, float* state) {
+    Camera& c = ((RefScene*)h)->scene->camera;
+    for (int i = 0; i < n; i++) {
+        float x = 0, y = 0;
+        bool ok = c.projectOntoCamera(Vec3(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), x, y);
+        out[3 * i] = ok ? 1.0f : 0.0f;
+        out[3 * i + 1] = x;
+        out[3 * i + 2] = y;
+    }
+    memcpy(state, c.projectionMatrix.m, 64);
+    memcpy(state + 16, c.cameraToView.m, 64);
+    state[32] = c.viewDirection.x; state[33] = c.viewDirection.y; state[34] = c.viewDirection.z;
+    state[35] = c.Afilm;
+}
+
+// AreaLight samplePositionFromLight + sampleDirectionFromLight + evaluate(-wi) (Lights.h:30-80) for
+// Scene::lights[li] with scripted draws: out = p.xyz, pdfPosition, wi.xyz, pdfDirection, Le.rgb,
+// draws used (lightTrace_init, Renderer.h:264-281).
+void ref_light_emit(void* h, int li, const float* draws, int ndraws, float* out) {
+    Light* L = ((RefScene*)h)->scene->lights[li];
+    ScriptSampler smp(draws, ndraws);
+    float pp = 0, pd = 0;
+    Vec3 p = L->samplePositionFromLight(smp, pp);
+    Vec3 wi = L->sampleDirectionFromLight(smp, pd);
+    Colour e = L->evaluate(-wi);
+    out[0] = p.x; out[1] = p.y; out[2] = p.z; out[3] = pp;
+    out[4] = wi.x; out[5] = wi.y; out[6] = wi.z; out[7] = pd;
+    out[8] = e.r; out[9] = e.g; out[10] = e.b; out[11] = (float)smp.i;
+}
+
 }  // extern "C"

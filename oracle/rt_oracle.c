@@ -7,6 +7,11 @@
  *   RayTracer::render / pathTracerTileBased / getTileID / renderTile  RTBase/Renderer.h:795-885
  *   RayTracer::pathTrace                                             RTBase/Renderer.h:328-392
  *   RayTracer::computeDirect                                         RTBase/Renderer.h:423-473
+ *   RayTracer::computeDirectMIS (+ convertPDFAreaToSolidAngle, balanceHeuristic) Renderer.h:408-557
+ *   RayTracer::adaptiveRender / adaptiveSampling / sampleTileWithWeight  RTBase/Renderer.h:583-749
+ *   RayTracer::lightTracer / lightTrace_init / lightTracePath / connectToCamera  Renderer.h:221-326
+ *   Camera::projectOntoCamera                                         RTBase/Scene.h:55-69
+ *   RayTracer::instantRadiosity / traceVPLs / VPLTracePath / computeVPLsContribution  Renderer.h:82-218
  *   Scene::traverse / visible / sampleLight / calculateShadingData   RTBase/Scene.h:107-203
  *   BVHNode::traverse / traverseVisible (left-first DFS, no culling) RTBase/Geometry.h:399-462
  *   AABB::rayAABB, Triangle::init / rayIntersect / sample / gNormal  RTBase/Geometry.h:72-184
@@ -135,6 +140,7 @@ struct or_scene {
     float* texels;
     int* light;
     rtg_camera cam;
+    rtg_camera_proj proj;
     int W, H;
 };
 
@@ -372,6 +378,18 @@ static Col compute_direct(const struct or_scene* s, const Shading* sd, Pcg* smp,
     return col(0.0f, 0.0f, 0.0f);
 }
 
+/* BSDF::PDF of the non-specular kinds: cosineHemispherePDF(frame.toLocal(wi)) (Materials.h:136-140) */
+static float bsdf_pdf(const Shading* sd, V3 wi) {
+    V3 wl = to_local(&sd->frame, wi);
+    return (float)((wl.z >= 0.0f) ? (wl.z / O_PI) : 0.0f);
+}
+/* convertPDFAreaToSolidAngle / balanceHeuristic (Renderer.h:408-422) */
+static float area_to_solid(float pdf_area, float dist2, float cos_theta) {
+    if (cos_theta > 0.0f) return pdf_area * dist2 / cos_theta;
+    return 0.0f;
+}
+static float balance(float pa, float pb) { return pa / (pa + pb); }
+
 /* BSDF::sample for the three effective behaviours */
 static V3 bsdf_sample(const struct or_scene* s, const Shading* sd, Pcg* smp, Col* refl, float* pdf) {
     const rtg_material* m = sd->bsdf;
@@ -411,6 +429,75 @@ static V3 bsdf_sample(const struct or_scene* s, const Shading* sd, Pcg* smp, Col
         *refl = cmuls(alb, 1.0f - R);
     }
     return to_world(&sd->frame, wi);
+}
+
+/* RayTracer::computeDirectMIS (Renderer.h:474-557) */
+static Col compute_direct_mis(const struct or_scene* s, const Shading* sd, Pcg* smp, Counts* c) {
+    if (is_spec(sd->bsdf)) return col(0.0f, 0.0f, 0.0f);
+    Col result = col(0.0f, 0.0f, 0.0f);
+    float pmf = 1.f / (float)s->nlight;
+    int li = (int)((float)s->nlight * pcg_next(smp));
+    if (s->nlight - 1 < li) li = s->nlight - 1;
+    int lt = s->light[li];
+    float pdf;
+    if (lt >= 0) {
+        const Tri* T = &s->tri[lt];
+        float r1 = pcg_next(smp);
+        float r2 = pcg_next(smp);
+        float alpha = 1 - sqrtf(r1);
+        float beta = r2 * sqrtf(r1);
+        float gamma = 1.0f - (alpha + beta);
+        pdf = 1.0f / T->area;
+        V3 p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+        const float* e = s->mat[T->mat].emission;
+        Col emitted = col(e[0], e[1], e[2]);
+        V3 wi = vsub(p, sd->x);
+        float l = vlen2(wi);
+        wi = vnorm(wi);
+        V3 gn = vmuls(T->nrm, vdot(T->n[0], T->nrm) > 0 ? 1.0f : -1.0f);
+        float cos_surface = win_max(vdot(wi, sd->sN), 0.0f);
+        float cos_light = win_max(-vdot(wi, gn), 0.0f);
+        float G = cos_surface * cos_light / l;
+        if (G > 0) {
+            if (scene_visible(s, sd->x, p, c)) {
+                float pdf_bsdf = bsdf_pdf(sd, wi);
+                float pdf_light = area_to_solid(pdf * pmf, l, cos_light);
+                float w = balance(pdf_light, pdf_bsdf);
+                result = cadd(result, cdivs(cmuls(cmuls(cmul(bsdf_eval(s, sd), emitted), G), w), pmf * pdf));
+            }
+        }
+    } else {
+        float q2 = pcg_next(smp);
+        float q1 = pcg_next(smp);
+        V3 wi = uniform_sample_sphere(q1, q2);
+        pdf = (float)(1.0f / (4.0f * O_PI));
+        Col emitted = env_eval(s, wi);
+        float G = win_max(vdot(wi, sd->sN), 0.0f);
+        if (G > 0) {
+            if (scene_visible(s, sd->x, vadd(sd->x, vmuls(wi, 10000.0f)), c))
+                return cdivs(cmuls(cmul(bsdf_eval(s, sd), emitted), G), pmf * pdf);
+        }
+    }
+    Col val;
+    float pdf_b;
+    V3 wib = bsdf_sample(s, sd, smp, &val, &pdf_b);
+    Ray r = ray_make(vadd(sd->x, vmuls(wib, O_EPS)), wib);
+    Isect is = scene_traverse(s, &r, c);
+    Shading sl = shading_data(s, &is, &r);
+    if (sl.t < FLT_MAX) {
+        if (is_light(sl.bsdf)) {
+            const float* e = sl.bsdf->emission;
+            Col emitted2 = col(e[0], e[1], e[2]);
+            V3 wi = vsub(sl.x, sd->x);
+            float dist2 = vlen2(wi);
+            wi = vnorm(wi);
+            float cos_light = win_max(0.0f, vdot(vneg(wi), sl.sN));
+            float pdf_light = area_to_solid(pdf * pmf, dist2, cos_light);
+            float w = balance(pdf_b, pdf_light);
+            result = cadd(result, cdivs(cmuls(cmuls(cmul(val, emitted2), win_max(0.0f, vdot(wib, sd->sN))), w), pdf_b));
+        }
+    }
+    return result;
 }
 
 /* RayTracer::pathTrace (Renderer.h:328-392) */
@@ -469,6 +556,17 @@ static Col direct_only(const struct or_scene* s, Ray* r, Pcg* smp, Counts* c) {
     return col(0.0f, 0.0f, 0.0f);
 }
 
+/* RayTracer::direct with computeDirectMIS in place of computeDirect */
+static Col direct_mis_only(const struct or_scene* s, Ray* r, Pcg* smp, Counts* c) {
+    Isect is = scene_traverse(s, r, c);
+    Shading sd = shading_data(s, &is, r);
+    if (sd.t < FLT_MAX) {
+        if (is_light(sd.bsdf)) return col(sd.bsdf->emission[0], sd.bsdf->emission[1], sd.bsdf->emission[2]);
+        return compute_direct_mis(s, &sd, smp, c);
+    }
+    return col(0.0f, 0.0f, 0.0f);
+}
+
 /* RayTracer::albedo (Renderer.h:558-571): emission, BSDF::evaluate(sd, (0,1,0)) or background */
 static Col albedo_only(const struct or_scene* s, Ray* r, Counts* c) {
     Isect is = scene_traverse(s, r, c);
@@ -504,6 +602,7 @@ static Col pixel_sample(const struct or_scene* s, uint32_t pixel, uint32_t sampl
     case RTG_INTEGRATOR_DIRECT: return direct_only(s, &r, &smp, c);
     case RTG_INTEGRATOR_ALBEDO: return albedo_only(s, &r, c);
     case RTG_INTEGRATOR_NORMALS: return normals_only(s, &r, c);
+    case RTG_INTEGRATOR_DIRECT_MIS: return direct_mis_only(s, &r, &smp, c);
     default: return path_trace(s, &r, &thr, 0, &smp, 1, c);
     }
 }
@@ -520,6 +619,7 @@ or_scene* or_create(const rtg_scene_desc* d, int max_depth) {
     s->env_tex = d->env_texture;
     s->max_depth = max_depth;
     s->cam = d->camera;
+    s->proj = d->projection;
     s->W = (int)d->camera.width;
     s->H = (int)d->camera.height;
     s->tri = (Tri*)calloc((size_t)s->ntri + 1, sizeof(Tri));
@@ -674,6 +774,263 @@ int or_render(or_scene* s, uint32_t first, uint32_t n_samples, uint64_t seed, co
     return 0;
 }
 
+/* RayTracer::adaptiveRender (Renderer.h:583-749): adaptiveSampling per tile (init samples, variance
+ * of the per-pixel means), weights = variance / total, sampleTileWithWeight (max((int)(sqrt(w) *
+ * max_samples), min_samples) samples, film += their mean). Sample indices: pass 1 uses first ..
+ * first+init-1, pass 2 first+init ... (the GPU build's convention for the deterministic sampler).
+ * tile_samples (optional) receives the pass-2 counts. Single-threaded. */
+int or_render_adaptive(or_scene* s, uint32_t first, uint64_t seed, uint32_t init, uint32_t max_samples,
+                       uint32_t min_samples, float* film, uint32_t* tile_samples) {
+    if (!s || !film || s->nlight <= 0 || init == 0) return -1;
+    const int TS = 32;
+    uint32_t tx = (uint32_t)(s->W + TS - 1) / TS, ty = (uint32_t)(s->H + TS - 1) / TS, nt = tx * ty;
+    float* var = (float*)calloc(nt, sizeof(float));
+    Col* est = (Col*)malloc(TS * TS * sizeof(Col));
+    for (uint32_t t = 0; t < nt; ++t) {
+        uint32_t x0 = (t % tx) * TS, y0 = (t / tx) * TS;
+        int n = 0;
+        for (uint32_t y = y0; y < y0 + TS && y < (uint32_t)s->H; ++y)
+            for (uint32_t x = x0; x < x0 + TS && x < (uint32_t)s->W; ++x) {
+                Col sum = col(0.0f, 0.0f, 0.0f);
+                for (uint32_t i = 0; i < init; ++i) sum = cadd(sum, pixel_sample(s, y * (uint32_t)s->W + x, first + i, seed, NULL));
+                est[n++] = cdivs(sum, (float)init);
+            }
+        Col gt = col(0.0f, 0.0f, 0.0f);
+        for (int i = 0; i < n; ++i) gt = cadd(gt, est[i]);
+        gt = cdivs(gt, (float)n);
+        Col sq = col(0.0f, 0.0f, 0.0f);
+        for (int i = 0; i < n; ++i) {
+            Col d = col(est[i].r - gt.r, est[i].g - gt.g, est[i].b - gt.b);
+            sq = cadd(sq, cmul(d, d));
+        }
+        var[t] = (((sq.r + sq.g) + sq.b) / 3.0f) / (float)(n - 1);
+    }
+    float total = 0.0f;
+    for (uint32_t t = 0; t < nt; ++t) total += var[t];
+    for (uint32_t t = 0; t < nt; ++t) {
+        float w = (total > 0.0f) ? var[t] / total : 0.0f;
+        w = sqrtf(w);
+        int smp = (int)(w * (float)max_samples);
+        smp = smp > (int)min_samples ? smp : (int)min_samples;
+        if (tile_samples) tile_samples[t] = (uint32_t)smp;
+        uint32_t x0 = (t % tx) * TS, y0 = (t / tx) * TS;
+        for (uint32_t y = y0; y < y0 + TS && y < (uint32_t)s->H; ++y)
+            for (uint32_t x = x0; x < x0 + TS && x < (uint32_t)s->W; ++x) {
+                uint32_t pix = y * (uint32_t)s->W + x;
+                Col c = col(0.0f, 0.0f, 0.0f);
+                for (int i = 0; i < smp; ++i) c = cadd(c, pixel_sample(s, pix, first + init + (uint32_t)i, seed, NULL));
+                c = cdivs(c, (float)smp);
+                float* f = film + (size_t)pix * 3;
+                f[0] = f[0] + c.r; f[1] = f[1] + c.g; f[2] = f[2] + c.b;
+            }
+    }
+    free(var);
+    free(est);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ light tracing (Renderer.h:221-326) */
+/* Camera::projectOntoCamera (Scene.h:55-69) */
+static int project_onto_camera(const struct or_scene* s, V3 p, float* x, float* y) {
+    const float* m = s->proj.camera_to_view;
+    V3 pv = v3(((p.x * m[0] + p.y * m[1]) + p.z * m[2]) + m[3], ((p.x * m[4] + p.y * m[5]) + p.z * m[6]) + m[7],
+               ((p.x * m[8] + p.y * m[9]) + p.z * m[10]) + m[11]);
+    const float* q = s->proj.proj;
+    V3 v1 = v3(((pv.x * q[0] + pv.y * q[1]) + pv.z * q[2]) + q[3], ((pv.x * q[4] + pv.y * q[5]) + pv.z * q[6]) + q[7],
+               ((pv.x * q[8] + pv.y * q[9]) + pv.z * q[10]) + q[11]);
+    float w = (((q[12] * pv.x) + (q[13] * pv.y)) + (q[14] * pv.z)) + q[15];
+    w = 1.0f / w;
+    V3 pp = vmuls(v1, w);
+    *x = (pp.x + 1.0f) * 0.5f;
+    *y = (pp.y + 1.0f) * 0.5f;
+    if (*x < 0 || *x > 1.0f || *y < 0 || *y > 1.0f) return 0;
+    *x = *x * s->cam.width;
+    *y = 1.0f - *y;
+    *y = *y * s->cam.height;
+    return 1;
+}
+/* (int)x with x86-64 cvttss2si semantics (NaN / out of range -> INT_MIN) */
+static int trunc_x86(float x) { return (x >= -2147483648.0f && x < 2147483648.0f) ? (int)x : (int)0x80000000; }
+/* Film::splat, BoxFilter (size 0): film[(int)y * W + (int)x] += L * 1 / 1 (Imaging.h:209-232) */
+static void splat(const struct or_scene* s, float* film, float x, float y, Col L) {
+    int px = trunc_x86(x), py = trunc_x86(y);
+    if (px >= 0 && (unsigned)px < (unsigned)s->W && py >= 0 && (unsigned)py < (unsigned)s->H) {
+        float* f = film + ((size_t)py * (unsigned)s->W + (unsigned)px) * 3;
+        f[0] = f[0] + ((L.r * 1.0f) / 1.0f);
+        f[1] = f[1] + ((L.g * 1.0f) / 1.0f);
+        f[2] = f[2] + ((L.b * 1.0f) / 1.0f);
+    }
+}
+/* RayTracer::connectToCamera (Renderer.h:236-262) */
+static void connect_to_camera(const struct or_scene* s, V3 p, V3 n, Col c, float* film, Counts* cnt) {
+    float x, y;
+    if (project_onto_camera(s, p, &x, &y)) {
+        float A = s->proj.a_film;
+        V3 org = v3(s->cam.origin[0], s->cam.origin[1], s->cam.origin[2]);
+        V3 dir = vsub(org, p);
+        float dist2 = vlen2(dir);
+        dir = vnorm(dir);
+        float cs = vdot(n, dir);
+        float cc = vdot(v3(s->proj.view_direction[0], s->proj.view_direction[1], s->proj.view_direction[2]), vneg(dir));
+        if (cs < 0.0f || cc < 0.0f) return;
+        float G = (cs * cc) / dist2;
+        if (!scene_visible(s, p, org, cnt)) return;
+        float We = 1 / (A * ((cc * cc) * (cc * cc)));
+        splat(s, film, x, y, cmuls(cmuls(c, We), G));
+    }
+}
+/* AreaLight: samplePositionFromLight (Triangle::sample) + sampleDirectionFromLight (Lights.h:63-80) */
+static void light_emit_sample(const struct or_scene* s, const Tri* T, Pcg* smp, V3* p, float* pdf_pos, V3* wi,
+                              float* pdf_dir, V3* gn) {
+    float r1 = pcg_next(smp);
+    float r2 = pcg_next(smp);
+    float alpha = 1 - sqrtf(r1);
+    float beta = r2 * sqrtf(r1);
+    float gamma = 1.0f - (alpha + beta);
+    *pdf_pos = 1.0f / T->area;
+    *p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+    float q2 = pcg_next(smp); /* cosineSampleHemisphere(sampler.next(), sampler.next()) */
+    float q1 = pcg_next(smp);
+    V3 wl = cosine_sample_hemisphere(q1, q2);
+    *pdf_dir = (float)((wl.z >= 0.0f) ? (wl.z / O_PI) : 0.0f);
+    *gn = vmuls(T->nrm, vdot(T->n[0], T->nrm) > 0 ? 1.0f : -1.0f);
+    Frame fr = frame_from(*gn);
+    *wi = to_world(&fr, wl);
+    (void)s;
+}
+/* RayTracer::lightTracePath (Renderer.h:292-326) */
+static void light_trace_path(const struct or_scene* s, Ray* r, Col thr, Col Le, Pcg* smp, float* film, Counts* c) {
+    for (;;) {
+        Isect is = scene_traverse(s, r, c);
+        Shading sd = shading_data(s, &is, r);
+        if (!(sd.t < FLT_MAX)) return;
+        if (is_light(sd.bsdf) || is_spec(sd.bsdf)) return;
+        V3 wi = vnorm(vsub(v3(s->cam.origin[0], s->cam.origin[1], s->cam.origin[2]), sd.x));
+        Col cl = cmul(cmul(thr, bsdf_eval(s, &sd)), Le);
+        connect_to_camera(s, sd.x, sd.sN, cl, film, c);
+        float rrp = win_min(clum(thr), 0.9f);
+        if (pcg_next(smp) < rrp) thr = cdivs(thr, rrp);
+        else return;
+        Col ind;
+        float pdf;
+        V3 wi2 = bsdf_sample(s, &sd, smp, &ind, &pdf);
+        thr = cdivs(cmuls(cmul(thr, ind), fabsf(vdot(wi2, sd.sN))), pdf);
+        *r = ray_make(vadd(sd.x, vmuls(wi2, O_EPS)), wi2);
+        (void)wi;
+    }
+}
+/* RayTracer::lightTracer + lightTrace_init (Renderer.h:221-235, 264-291): W*H light paths per frame,
+ * path i drawing from the PCG stream keyed (seed, i, frame). */
+int or_render_light(or_scene* s, uint32_t first, uint32_t n_frames, uint64_t seed, float* film) {
+    if (!s || !film || s->nlight <= 0) return -1;
+    for (uint32_t f = first; f < first + n_frames; ++f) {
+        for (uint32_t i = 0; i < (uint32_t)(s->W * s->H); ++i) {
+            Pcg smp;
+            pcg_init(&smp, seed, ((uint64_t)i << 16) | f);
+            float pmf = 1.f / (float)s->nlight;
+            int li = (int)((float)s->nlight * pcg_next(&smp));
+            if (s->nlight - 1 < li) li = s->nlight - 1;
+            int lt = s->light[li];
+            if (lt < 0) continue; /* light->isArea() */
+            const Tri* T = &s->tri[lt];
+            V3 p, wi, gn;
+            float pdf_pos, pdf_dir;
+            light_emit_sample(s, T, &smp, &p, &pdf_pos, &wi, &pdf_dir, &gn);
+            float cos_t = vdot(gn, wi);
+            const float* e = s->mat[T->mat].emission;
+            Col ev = vdot(vneg(wi), gn) < 0 ? col(e[0], e[1], e[2]) : col(0.0f, 0.0f, 0.0f); /* evaluate(-wi) */
+            Col Le = cdivs(cmuls(ev, cos_t), (pmf * pdf_dir) * pdf_pos);
+            connect_to_camera(s, p, gn, Le, film, NULL);
+            Ray r = ray_make(p, wi);
+            light_trace_path(s, &r, col(1.0f, 1.0f, 1.0f), Le, &smp, film, NULL);
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ instant radiosity (Renderer.h:82-218) */
+typedef struct { V3 x, n; Col Le; } Vpl;
+typedef struct { Vpl* v; int n, cap; } VplList;
+static void vpl_push(VplList* l, V3 x, V3 n, Col Le) {
+    if (l->n == l->cap) {
+        l->cap = l->cap ? 2 * l->cap : 64;
+        l->v = (Vpl*)realloc(l->v, (size_t)l->cap * sizeof(Vpl));
+    }
+    l->v[l->n].x = x; l->v[l->n].n = n; l->v[l->n].Le = Le;
+    l->n++;
+}
+/* RayTracer::VPLTracePath (Renderer.h:183-218, recursion unrolled) */
+static void vpl_trace_path(const struct or_scene* s, Ray* r, Col thr, Col Le, Pcg* smp, VplList* out) {
+    for (;;) {
+        Isect is = scene_traverse(s, r, NULL);
+        Shading sd = shading_data(s, &is, r);
+        if (!(sd.t < FLT_MAX)) return;
+        if (!is_light(sd.bsdf) && !is_spec(sd.bsdf))
+            vpl_push(out, sd.x, sd.sN, cmuls(cmul(cmul(thr, Le), bsdf_eval(s, &sd)), fabsf(vdot(vneg(r->dir), sd.sN))));
+        float rrp = win_min(clum(thr), 0.9f);
+        if (pcg_next(smp) < rrp) thr = cdivs(thr, rrp);
+        else return;
+        Col val;
+        float pdf;
+        V3 wi = bsdf_sample(s, &sd, smp, &val, &pdf);
+        thr = cdivs(cmuls(cmul(thr, val), fabsf(vdot(wi, sd.sN))), pdf);
+        *r = ray_make(vadd(sd.x, vmuls(wi, O_EPS)), wi);
+    }
+}
+/* RayTracer::instantRadiosity: traceVPLs (n_vpl paths, path i keyed (seed, i, frame)), then per pixel
+ * the first hit and computeVPLsContribution (Renderer.h:101-156). */
+int or_render_ir(or_scene* s, uint32_t first, uint32_t n_frames, uint64_t seed, uint32_t n_vpl, float* film) {
+    if (!s || !film || s->nlight <= 0 || n_vpl == 0) return -1;
+    for (uint32_t f = first; f < first + n_frames; ++f) {
+        VplList vl = {NULL, 0, 0};
+        for (uint32_t i = 0; i < n_vpl; ++i) {
+            Pcg smp;
+            pcg_init(&smp, seed, ((uint64_t)i << 16) | f);
+            float pmf = 1.f / (float)s->nlight;
+            int li = (int)((float)s->nlight * pcg_next(&smp));
+            if (s->nlight - 1 < li) li = s->nlight - 1;
+            int lt = s->light[li];
+            if (lt < 0) continue;
+            const Tri* T = &s->tri[lt];
+            V3 p, wi, gn;
+            float pdf_pos, pdf_dir;
+            light_emit_sample(s, T, &smp, &p, &pdf_pos, &wi, &pdf_dir, &gn);
+            const float* e = s->mat[T->mat].emission;
+            Col ev = vdot(vneg(wi), gn) < 0 ? col(e[0], e[1], e[2]) : col(0.0f, 0.0f, 0.0f);
+            float den = (pmf * pdf_pos) * (float)n_vpl;
+            vpl_push(&vl, p, gn, cdivs(ev, den));
+            Col Le = cdivs(cmuls(ev, vdot(wi, gn)), den);
+            Ray r = ray_make(p, wi);
+            vpl_trace_path(s, &r, col(1.0f, 1.0f, 1.0f), Le, &smp, &vl);
+        }
+        for (uint32_t y = 0; y < (uint32_t)s->H; ++y)
+            for (uint32_t x = 0; x < (uint32_t)s->W; ++x) {
+                Ray r = camera_ray(s, x + 0.5f, y + 0.5f);
+                Isect is = scene_traverse(s, &r, NULL);
+                Shading sd = shading_data(s, &is, &r);
+                if (!(sd.t < FLT_MAX)) continue;
+                Col sum = col(0.0f, 0.0f, 0.0f);
+                if (!is_light(sd.bsdf) && !is_spec(sd.bsdf)) {
+                    for (int j = 0; j < vl.n; ++j) {
+                        V3 dir = vsub(vl.v[j].x, sd.x);
+                        float dist2 = vlen2(dir);
+                        if (dist2 < 1e-4f) continue;
+                        dir = vnorm(dir);
+                        float cv = vdot(vl.v[j].n, vneg(dir));
+                        float cx = vdot(sd.sN, dir);
+                        if (cv <= 0.0f || cx <= 0.0f) continue;
+                        float G = (cv * cx) / dist2;
+                        if (!scene_visible(s, sd.x, vl.v[j].x, NULL)) continue;
+                        sum = cadd(sum, cmuls(cmul(vl.v[j].Le, bsdf_eval(s, &sd)), G));
+                    }
+                }
+                splat(s, film, x + 0.5f, y + 0.5f, sum);
+            }
+        free(vl.v);
+    }
+    return 0;
+}
+
 /* Ray queries with the reference traversal (IntersectionData / Scene::visible semantics).
  * rays: n*8 (o.xyz, tmax, dir.xyz, pad); hits n*4 (t, id bits, alpha, beta). */
 int or_trace_closest(or_scene* s, const float* rays, uint32_t n, float* hits) {
@@ -707,6 +1064,38 @@ int or_camera_rays(or_scene* s, const uint32_t* pixels, uint32_t n, float* out) 
         out[i * 6] = r.o.x; out[i * 6 + 1] = r.o.y; out[i * 6 + 2] = r.o.z;
         out[i * 6 + 3] = r.dir.x; out[i * 6 + 4] = r.dir.y; out[i * 6 + 5] = r.dir.z;
     }
+    return 0;
+}
+
+/* Probes of the light-tracing pieces (tests): projectOntoCamera on points -> (ok, x, y); the
+ * AreaLight emission sample of lights[li] from 4 scripted draws -> p, pdfPosition, wi, pdfDirection,
+ * evaluate(-wi). */
+int or_camera_project(or_scene* s, const float* pts, uint32_t n, float* out) {
+    for (uint32_t i = 0; i < n; ++i) {
+        float x = 0, y = 0;
+        int ok = project_onto_camera(s, v3(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]), &x, &y);
+        out[3 * i] = ok ? 1.0f : 0.0f; out[3 * i + 1] = x; out[3 * i + 2] = y;
+    }
+    return 0;
+}
+int or_light_emit(or_scene* s, int li, const float* draws, float* out) {
+    int lt = s->light[li];
+    if (lt < 0) return -1;
+    const Tri* T = &s->tri[lt];
+    /* a stream whose next four draws are the scripted ones is not expressible with PCG: restate
+     * the sampling here with the draws in call order (r1, r2, then the direction's q2, q1) */
+    float r1 = draws[0], r2 = draws[1], q2 = draws[2], q1 = draws[3];
+    float alpha = 1 - sqrtf(r1), beta = r2 * sqrtf(r1), gamma = 1.0f - (alpha + beta);
+    V3 p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+    V3 wl = cosine_sample_hemisphere(q1, q2);
+    V3 gn = vmuls(T->nrm, vdot(T->n[0], T->nrm) > 0 ? 1.0f : -1.0f);
+    Frame fr = frame_from(gn);
+    V3 wi = to_world(&fr, wl);
+    const float* e = s->mat[T->mat].emission;
+    Col ev = vdot(vneg(wi), gn) < 0 ? col(e[0], e[1], e[2]) : col(0.0f, 0.0f, 0.0f);
+    out[0] = p.x; out[1] = p.y; out[2] = p.z; out[3] = 1.0f / T->area;
+    out[4] = wi.x; out[5] = wi.y; out[6] = wi.z; out[7] = (float)((wl.z >= 0.0f) ? (wl.z / O_PI) : 0.0f);
+    out[8] = ev.r; out[9] = ev.g; out[10] = ev.b; out[11] = 4.0f;
     return 0;
 }
 

@@ -12,6 +12,7 @@ LIB_DIR = os.path.join(_HERE, "lib")
 RTG_MAT_DIFFUSE, RTG_MAT_LAMBERT, RTG_MAT_MIRROR, RTG_MAT_GLASS = 0, 1, 2, 3
 RTG_OPT_CULL, RTG_OPT_COUNT, RTG_OPT_TIMING, RTG_OPT_BVH2 = 1, 2, 4, 8
 RTG_INTEGRATOR_PATH, RTG_INTEGRATOR_DIRECT, RTG_INTEGRATOR_ALBEDO, RTG_INTEGRATOR_NORMALS = 0, 1, 2, 3
+RTG_INTEGRATOR_DIRECT_MIS = 4
 
 f32p = C.POINTER(C.c_float)
 u32p = C.POINTER(C.c_uint32)
@@ -21,6 +22,11 @@ i32p = C.POINTER(C.c_int32)
 class rtg_camera(C.Structure):
     _fields_ = [("inv_proj", C.c_float * 16), ("camera", C.c_float * 16), ("origin", C.c_float * 3),
                 ("width", C.c_float), ("height", C.c_float)]
+
+
+class rtg_camera_proj(C.Structure):
+    _fields_ = [("proj", C.c_float * 16), ("camera_to_view", C.c_float * 16), ("view_direction", C.c_float * 3),
+                ("a_film", C.c_float)]
 
 
 class rtg_material(C.Structure):
@@ -38,7 +44,8 @@ class rtg_scene_desc(C.Structure):
                 ("node_links", i32p), ("n_materials", C.c_uint32),
                 ("materials", C.POINTER(rtg_material)), ("n_textures", C.c_uint32),
                 ("textures", C.POINTER(rtg_texture)), ("env_texture", C.c_int32),
-                ("n_lights", C.c_uint32), ("lights", i32p), ("camera", rtg_camera)]
+                ("n_lights", C.c_uint32), ("lights", i32p), ("camera", rtg_camera),
+                ("projection", rtg_camera_proj)]
 
 
 class rtg_stats(C.Structure):
@@ -74,6 +81,9 @@ RTG_EXPORTS = [
     ("rtg_render", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32]),
     ("rtg_render_async", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32, C.c_void_p]),
     ("rtg_synchronize", C.c_int, [C.c_void_p]),
+    ("rtg_render_light", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64]),
+    ("rtg_render_instant_radiosity", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32]),
+    ("rtg_render_adaptive", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, u32p]),
     ("rtg_film_read", C.c_int, [C.c_void_p, f32p, u32p]),
     ("rtg_film_copy_device", C.c_int, [C.c_void_p, C.c_void_p]),
     ("rtg_film_load", C.c_int, [C.c_void_p, f32p, C.c_uint32]),

@@ -23,7 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RTG_ARCH", "gfx950")
 
 HOST_SRC = ["host/image_io.cpp", "host/jpeg_decode.cpp", "host/gem_json.cpp", "host/scene_front.cpp"]
-DEVICE_SRC = ["device/rtg_kernels.hip"]
+DEVICE_SRC = ["device/rtg_kernels.hip", "device/rtg_light.hip"]
 
 
 def _newer(out, deps):

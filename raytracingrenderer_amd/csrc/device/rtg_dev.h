@@ -345,6 +345,18 @@ RTG_D v3 bsdf_sample(int kind, float int_ior, float ext_ior, v3 alb, const frame
     return to_world(fr, wi);
 }
 
+// BSDF::PDF of the non-specular kinds: cosineHemispherePDF(shadingData.frame.toLocal(wi))
+// (Materials.h:136-140, 227-232, 349-354, 394-399, 447-452; Sampling.h:52-56). Only z of toLocal is used.
+RTG_D float bsdf_pdf_lambert(const frame& fr, v3 wi) {
+    const float z = dot(wi, fr.w);
+    return (z >= 0.0f) ? (float)((double)z / RTM_PI) : 0.0f;
+}
+// RayTracer::convertPDFAreaToSolidAngle / balanceHeuristic (Renderer.h:411-422)
+RTG_D float pdf_area_to_solid(float pdf_area, float dist2, float cos_theta) {
+    return cos_theta > 0.0f ? (pdf_area * dist2) / cos_theta : 0.0f;
+}
+RTG_D float balance_heuristic(float pa, float pb) { return pa / (pa + pb); }
+
 // ------------------------------------------------------------------ intersection
 // AABB::rayAABB with the reference's exact arithmetic; returns pass/fail.
 RTG_D bool slab_exact(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, v3 o, v3 inv) {

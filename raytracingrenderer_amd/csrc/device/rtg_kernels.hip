@@ -20,8 +20,7 @@
 // which is what the reference's left-first DFS with strict '<' keeps; box tests use the reference's
 // exact slab arithmetic, and distance culling only removes boxes whose conservatively inflated entry
 // is beyond the current hit.
-#include "rtg_dev.h"
-#include "../../../include/rtg.h"
+#include "rtg_internal.h"
 
 #include <hip/hip_runtime.h>
 
@@ -33,88 +32,6 @@
 #include <cstring>
 #include <string>
 #include <vector>
-
-using namespace rtgd;
-
-#define RTG_TB 256          // threads per block (4 waves)
-#define RTG_POP ((int)0x80000001)  // "pop the stack" marker inside one traversal step
-#ifndef RTG_STACK
-#define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (24 KB per block)
-#endif
-#ifndef RTG_POSTPONE
-#define RTG_POSTPONE 32     // >0: park a reached leaf and keep walking; run the leaves of a wave together
-#endif                      //     once this many lanes hold one (or no lane can walk on)
-#ifndef RTG_DRAIN_LEAF
-#define RTG_DRAIN_LEAF 1    // once the queue is empty, run the leaf phase whenever a lane has parked a
-#endif                      //     leaf (the drain is latency-bound: lanes should not wait for each other)
-#ifndef RTG_REFILL
-#define RTG_REFILL 16       // refill idle lanes once at least this many are idle (the setup code then
-#endif                      // runs with more lanes per execution)
-#ifndef RTG_TRACE_WPE
-#define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel
-#endif
-#define RTG_CULL_REL 1.52587890625e-05f  // 2^-16 relative inflation for distance culling
-#ifndef RTG_SHADE_WAVES
-#define RTG_SHADE_WAVES 4                // min waves per SIMD for k_shade (register budget)
-#endif
-
-struct __align__(16) Counters { unsigned n_ext, n_shadow, f_ext, f_shadow, f_shade, pad0, pad1, pad2; };
-
-// Queues hold path ids only; ray payloads live in per-path arrays (written in place by k_shade),
-// so compaction moves 4 bytes per ray and needs one atomic per 256 paths.
-// One traversal launch serves two ray sets: extension (closest-hit) rays take work indices
-// [0, nc) and NEE shadow (any-hit) rays [nc, nc + ns). Each lane carries its ray's kind.
-struct TraceIO {
-    const unsigned* queue;     // closest: path ids to trace
-    const float4* ray_o;       // closest: [pid] origin.xyz
-    const float4* ray_d;       // closest: [pid] direction.xyz
-    const unsigned* count;     // closest: number of rays (device; null = none)
-    float4* hits;              // closest-hit output [pid]
-    const unsigned* squeue;    // any-hit: path ids
-    const float4* sray_o;      // any-hit: [pid] origin.xyz, w = maxT
-    const float4* sray_d;      // any-hit: [pid] direction.xyz
-    const float4* sray_c;      // any-hit: [pid] NEE value copied to contrib[pid] when visible
-    const unsigned* scount;    // any-hit: number of rays (device; null = none)
-    float4* contrib;           // any-hit: this bounce's contribution plane [pid]
-    int* visible;              // any-hit query output [pid] (instead of contrib)
-    unsigned* fetch;           // work counter over both sets (device, zeroed)
-    int* ovf;                  // global stack overflow [level][thread]
-    unsigned long long* stats; // [0,1] closest / [4,5] any-hit: box tests, triangle tests (COUNT)
-    int cull;
-    int wide;                  // traverse the 4-wide tree when the ray allows it
-    unsigned long long* wtime; // diagnostics (RTG_WAVETIME): per wave start / drained / exit clock
-};
-
-struct ChunkArgs {
-    const unsigned* pixlist;   // local pixel -> pixel index (y*W + x)
-    unsigned npix, ns, s0, P;
-    unsigned long long seed;
-    int max_depth;
-    int mode;                  // RTG_INTEGRATOR_* (first-hit estimators never continue a path)
-    DevCamera cam;
-};
-
-struct PathBufs {
-    float4* thr;               // [P] throughput
-    unsigned long long* rng;   // [P] PCG state
-    int* meta;                 // [P] nterms | canHitLight << 8
-    float4* contrib;           // [maxb][P] per-vertex radiance terms
-    float4* ray_o;             // [P] current extension ray origin
-    float4* ray_d;             // [P] current extension ray direction
-    float4* hits;              // [P] its closest hit (t, id, alpha, beta)
-    float4* sh_o;              // [P] NEE shadow ray origin + maxT
-    float4* sh_d;              // [P] NEE shadow ray direction
-    float4* sh_c;              // [P] NEE value thr * Ld if visible
-    unsigned* q[2];            // extension queues of path ids (ping-pong)
-    unsigned* shq;             // shadow queue of path ids
-    Counters* ctr;             // [maxb + 1]
-};
-
-static __device__ __forceinline__ int lane_id() { return __lane_id(); }
-static __device__ __forceinline__ unsigned prefix_lt(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
-
 
 // ------------------------------------------------------------------ traversal
 // Persistent lanes with per-lane ray replacement: a wave takes 64 ray indices at a time from the
@@ -539,6 +456,9 @@ __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
 }
 
 // ------------------------------------------------------------------ shade
+// ALT = false: pathTrace only (RayTracer::render's estimator; the other modes compile away).
+// ALT = true: every per-pixel estimator of rtg_set_integrator, selected by a.mode.
+template <bool ALT>
 __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
     __shared__ unsigned s_cnt[2][RTG_TB / 64];
     __shared__ unsigned s_base[2];
@@ -566,11 +486,40 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             uint64_t st = p.rng[pid];
             v3 c;
             int nterms = b + 1;
-            if (!(h.x < RTG_FLT_MAX)) {
+            if (ALT && a.mode == RTG_INTEGRATOR_DIRECT_MIS && b == 1) {
+                // computeDirectMIS, second half (Renderer.h:520-553): the BSDF-sampled ray's hit.
+                // thr = (bsdf value, bsdf pdf); scratch planes 2/3 = (x, light pdf * pmf) and
+                // (max(0, wi.sN), env-sample flag); contrib plane 0 .w = 1 iff an env NEE sample was
+                // visible, in which case the reference has already returned (:508-516).
+                const float4 A = p.contrib[(size_t)2 * a.P + pid], B = p.contrib[(size_t)3 * a.P + pid];
+                const float4 c0 = p.contrib[pid];
+                c = mk(0.0f, 0.0f, 0.0f);
+                if (B.y != 0.0f && c0.w == 1.0f) {
+                    nterms = 1;
+                } else if (h.x < RTG_FLT_MAX) {
+                    const int tri = __float_as_int(h.y);
+                    const DevShade S = s.shade[tri];
+                    const DevMat M = s.mats[__float_as_int(S.d.w)];
+                    if (M.is_light) {
+                        const float alpha = h.z, beta = h.w, gamma = 1.0f - (alpha + beta);
+                        const v3 x2 = add(o, muls(d, h.x));
+                        const v3 n0 = mk(S.a.x, S.a.y, S.a.z), n1 = mk(S.a.w, S.b.x, S.b.y), n2 = mk(S.b.z, S.b.w, S.c.x);
+                        v3 sn2 = normalize(add(add(muls(n0, alpha), muls(n1, beta)), muls(n2, gamma)));
+                        if (M.two_sided && dot(neg(d), sn2) < 0) sn2 = neg(sn2);
+                        v3 wi = sub(x2, mk(A.x, A.y, A.z));
+                        const float dist2 = length_sq(wi);
+                        wi = normalize(wi);
+                        const float cos_l = wmax(0.0f, dot(neg(wi), sn2));
+                        const float pls = pdf_area_to_solid(A.w, dist2, cos_l);
+                        const float wgt = balance_heuristic(thr4.w, pls);
+                        c = divs(muls(muls(mul(thr, mk(M.emission.x, M.emission.y, M.emission.z)), B.x), wgt), thr4.w);
+                    }
+                }
+            } else if (!(h.x < RTG_FLT_MAX)) {
                 // miss: background->evaluate(r.dir), not weighted by throughput (Renderer.h:390);
                 // direct() and viewNormals() return black
-                c = (a.mode == RTG_INTEGRATOR_PATH || a.mode == RTG_INTEGRATOR_ALBEDO) ? background(s, d)
-                                                                                     : mk(0.0f, 0.0f, 0.0f);
+                c = (!ALT || a.mode == RTG_INTEGRATOR_PATH || a.mode == RTG_INTEGRATOR_ALBEDO) ? background(s, d)
+                                                                                             : mk(0.0f, 0.0f, 0.0f);
             } else {
                 const int tri = __float_as_int(h.y);
                 const float alpha = h.z, beta = h.w, gamma = 1.0f - (alpha + beta);
@@ -585,14 +534,93 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                 const v3 wo = neg(d);
                 if (M.two_sided && dot(wo, sn) < 0) sn = neg(sn);
                 const frame fr = frame_from(sn);
-                if (a.mode == RTG_INTEGRATOR_NORMALS) {  // viewNormals (Renderer.h:572-582)
+                if (ALT && a.mode == RTG_INTEGRATOR_NORMALS) {  // viewNormals (Renderer.h:572-582)
                     c = mk(fabsf(sn.x), fabsf(sn.y), fabsf(sn.z));
                 } else if (M.is_light) {
-                    c = a.mode != RTG_INTEGRATOR_PATH ? mk(M.emission.x, M.emission.y, M.emission.z)  // emit()
+                    c = (ALT && a.mode != RTG_INTEGRATOR_PATH) ? mk(M.emission.x, M.emission.y, M.emission.z)  // emit()
                         : can_hit ? mul(thr, mk(M.emission.x, M.emission.y, M.emission.z)) : mk(0.0f, 0.0f, 0.0f);
-                } else if (a.mode == RTG_INTEGRATOR_ALBEDO) {  // BSDF::evaluate(sd, (0,1,0))
+                } else if (ALT && a.mode == RTG_INTEGRATOR_ALBEDO) {  // BSDF::evaluate(sd, (0,1,0))
                     const v3 alb = tex_sample(s, M.tex, tu, tv);
                     c = M.kind == RTG_MAT_MIRROR ? alb : (M.kind == RTG_MAT_GLASS ? mk(0.0f, 0.0f, 0.0f) : divs(alb, RTG_PI_F));
+                } else if (ALT && a.mode == RTG_INTEGRATOR_DIRECT_MIS) {
+                    // computeDirectMIS, first half (Renderer.h:474-519): one light sample weighted by
+                    // the balance heuristic (its shadow ray), then one BSDF sample (its extension ray)
+                    c = mk(0.0f, 0.0f, 0.0f);
+                    if (!(M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS)) {
+                        const int nl = s.n_lights;
+                        const float pmf = 1.f / (float)nl;
+                        int li = (int)((float)nl * pcg_next(st, inc));
+                        li = (nl - 1) < li ? (nl - 1) : li;
+                        const DevLight L = s.lights[li];
+                        const v3 f = divs(tex_sample(s, M.tex, tu, tv), RTG_PI_F);  // BSDF::evaluate
+                        float pdf;
+                        float env_flag = 0.0f;
+                        if (__float_as_int(L.v1t.w) == 0) {
+                            const float r1 = pcg_next(st, inc);
+                            const float r2 = pcg_next(st, inc);
+                            const float la = 1 - sqrtf(r1);
+                            const float lb = r2 * sqrtf(r1);
+                            const float lg = 1.0f - (la + lb);
+                            pdf = 1.0f / L.v0a.w;
+                            const v3 p2 = add(add(muls(mk(L.v0a.x, L.v0a.y, L.v0a.z), la), muls(mk(L.v1t.x, L.v1t.y, L.v1t.z), lb)),
+                                              muls(mk(L.v2.x, L.v2.y, L.v2.z), lg));
+                            v3 wi = sub(p2, x);
+                            const float l2 = length_sq(wi);
+                            wi = normalize(wi);
+                            const float cos_s = wmax(dot(wi, sn), 0.0f);
+                            const float cos_l = wmax(-dot(wi, mk(L.gn.x, L.gn.y, L.gn.z)), 0.0f);
+                            const float g = (cos_s * cos_l) / l2;
+                            if (g > 0) {
+                                const float pdf_b = bsdf_pdf_lambert(fr, wi);
+                                const float pls = pdf_area_to_solid(pdf * pmf, l2, cos_l);
+                                const float wgt = balance_heuristic(pls, pdf_b);
+                                const v3 r = add(mk(0.0f, 0.0f, 0.0f),
+                                                 divs(muls(muls(mul(f, mk(L.em.x, L.em.y, L.em.z)), g), wgt), pmf * pdf));
+                                v3 sd = sub(p2, x);
+                                const float maxt = sqrtf(length_sq(sd)) - (2.0f * RTG_EPS);
+                                sd = normalize(sd);
+                                const v3 so = add(x, muls(sd, RTG_EPS));
+                                p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
+                                p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 0.0f);
+                                p.sh_c[pid] = make_float4(r.x, r.y, r.z, 0.0f);
+                                want_sh = true;
+                            }
+                        } else {
+                            const float q2 = pcg_next(st, inc);
+                            const float q1 = pcg_next(st, inc);
+                            const v3 wi = uniform_sample_sphere(q1, q2);
+                            pdf = uniform_sphere_pdf();
+                            const float g = wmax(dot(wi, sn), 0.0f);
+                            if (g > 0) {
+                                const v3 r = divs(muls(mul(f, env_eval(s, wi)), g), pmf * pdf);
+                                const v3 p2 = add(x, muls(wi, 10000.0f));
+                                v3 sd = sub(p2, x);
+                                const float maxt = sqrtf(length_sq(sd)) - (2.0f * RTG_EPS);
+                                sd = normalize(sd);
+                                const v3 so = add(x, muls(sd, RTG_EPS));
+                                p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
+                                p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 0.0f);
+                                p.sh_c[pid] = make_float4(r.x, r.y, r.z, 1.0f);  // .w: env sample visible
+                                want_sh = true;
+                                env_flag = 1.0f;
+                            }
+                        }
+                        // BSDF sample and its ray (Renderer.h:520-525)
+                        v3 val;
+                        float pdf_b;
+                        PcgSampler smp{st, inc};
+                        const v3 wib = bsdf_sample(M.kind, M.int_ior, M.ext_ior, tex_sample(s, M.tex, tu, tv), fr, wo, smp,
+                                                   val, pdf_b);
+                        st = smp.s;
+                        const v3 no = add(x, muls(wib, RTG_EPS));
+                        p.ray_o[pid] = make_float4(no.x, no.y, no.z, 0.0f);
+                        p.ray_d[pid] = make_float4(wib.x, wib.y, wib.z, 0.0f);
+                        p.thr[pid] = make_float4(val.x, val.y, val.z, pdf_b);
+                        p.contrib[(size_t)2 * a.P + pid] = make_float4(x.x, x.y, x.z, pdf * pmf);
+                        p.contrib[(size_t)3 * a.P + pid] = make_float4(wmax(0.0f, dot(wib, sn)), env_flag, 0.0f, 0.0f);
+                        want_ext = true;
+                        nterms = 2;
+                    }
                 } else {
                     const bool spec = M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS;
                     // ---- computeDirect (Renderer.h:423-473)
@@ -646,7 +674,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                     }
                     // direct = thr * Ld, with Ld = 0 until the shadow ray says visible
                     c = mul(thr, mk(0.0f, 0.0f, 0.0f));
-                    if (a.mode == RTG_INTEGRATOR_PATH && b <= a.max_depth) {
+                    if ((!ALT || a.mode == RTG_INTEGRATOR_PATH) && b <= a.max_depth) {
                         const float rrp = wmin(lum(thr), 0.9f);
                         if (pcg_next(st, inc) < rrp) {
                             thr = divs(thr, rrp);
@@ -725,6 +753,16 @@ __global__ __launch_bounds__(RTG_TB) void k_accumulate(ChunkArgs a, PathBufs p, 
     film[(size_t)pixel * 3 + 2] = fb;
 }
 
+// sampleTileWithWeight's splat (Renderer.h:661-670): film += (sum of n samples) / (float)n for the
+// listed pixels; tmp holds the per-pixel sums of a scratch render.
+__global__ __launch_bounds__(RTG_TB) void k_fold_mean(const unsigned* pixlist, unsigned npix, const float* tmp,
+                                                      float count, float* film) {
+    const unsigned lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= npix) return;
+    const size_t q = (size_t)pixlist[lp] * 3;
+    for (int c = 0; c < 3; ++c) film[q + c] = film[q + c] + (tmp[q + c] / count);
+}
+
 // BSDF probe: the exact device BSDF code on scripted inputs (unit parity vs RTBase's BSDF classes).
 // in: 20 floats per case = kind, int_ior, ext_ior, albedo.rgb (1x1 texture), sN.xyz, wo.xyz, tu, tv,
 //     draws[4], pad[2]; out: 11 floats = wi.xyz, refl.rgb, pdf, draws used, evaluate.rgb
@@ -762,73 +800,7 @@ __global__ void k_tally(const Counters* ctr, int maxb, unsigned long long* stats
 }
 
 // ================================================================== host side (C-ABI)
-static thread_local std::string g_err;
-
-#define HIPOK(expr)                                                                          \
-    do {                                                                                     \
-        hipError_t e_ = (expr);                                                              \
-        if (e_ != hipSuccess) {                                                              \
-            g_err = std::string(#expr) + ": " + hipGetErrorString(e_);                       \
-            return RTG_ERR_HIP;                                                              \
-        }                                                                                    \
-    } while (0)
-
-template <class T>
-static int dev_upload(T** dst, const std::vector<T>& src) {
-    *dst = nullptr;
-    size_t bytes = std::max<size_t>(src.size(), 1) * sizeof(T);
-    HIPOK(hipMalloc((void**)dst, bytes));
-    if (!src.empty()) HIPOK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
-    return RTG_OK;
-}
-
-struct rtg_handle {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    int W = 0, H = 0;
-    uint32_t spp = 0;
-    int max_depth = 4, cull = 1, count = 0, timing = 0;
-    uint32_t max_paths = 1u << 26;  // 64M paths in flight (~17 GB at depth 4 of 288 GB HBM)
-    int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0, shade_blocks = 0;
-    uint32_t bvh_depth = 0;
-    SceneView sv{};
-    DevCamera cam{};
-    DevNode* d_nodes = nullptr;
-    DevNodeW* d_nodesw = nullptr;
-    DevNodeQ* d_nodesq = nullptr;
-    float4* d_leafbox = nullptr;
-    int usew = 0, wide = 1;
-    int integrator = RTG_INTEGRATOR_PATH;
-    uint32_t wide_depth = 0;  // wide levels on the longest root-to-leaf path
-    DevTri* d_tris = nullptr;
-    DevTri48* d_tris48 = nullptr;
-    DevShade* d_shade = nullptr;
-    DevMat* d_mats = nullptr;
-    DevLight* d_lights = nullptr;
-    DevTex* d_texinfo = nullptr;
-    float* d_texels = nullptr;
-    float* d_film = nullptr;
-    // chunk buffers
-    // two chunk pipelines (buffers, stream, overflow region each): pipeline 1 runs on stream2
-    size_t cap_P[2] = {0, 0};
-    int cap_maxb[2] = {0, 0};
-    PathBufs pb[2]{};
-    hipStream_t stream2 = nullptr;
-    int pipes = 1, stagger = 2;
-    hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};  // fork, stagger, join, accumulate-order
-    unsigned* d_pix = nullptr;
-    size_t cap_pix = 0;
-    std::vector<uint32_t> pix_key;
-    unsigned npix = 0;
-    int* d_ovf = nullptr;
-    size_t cap_ovf = 0;
-    unsigned* d_qctr = nullptr;  // query-API counters [4]
-    unsigned long long* d_stats = nullptr;
-    rtg_stats stats{};
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    std::vector<hipEvent_t> kev;  // per-launch timing events (timing mode)
-};
-
+thread_local std::string g_err;
 static void free_chunk(rtg_handle* h, int i) {
     PathBufs& p = h->pb[i];
     (void)hipFree(p.thr); (void)hipFree(p.rng); (void)hipFree(p.meta); (void)hipFree(p.contrib);
@@ -840,7 +812,7 @@ static void free_chunk(rtg_handle* h, int i) {
     h->cap_maxb[i] = 0;
 }
 
-static int ensure_chunk(rtg_handle* h, int i, size_t P, int maxb) {
+int ensure_chunk(rtg_handle* h, int i, size_t P, int maxb) {
     if (P <= h->cap_P[i] && maxb <= h->cap_maxb[i]) return RTG_OK;
     free_chunk(h, i);
     PathBufs& p = h->pb[i];
@@ -863,7 +835,7 @@ static int ensure_chunk(rtg_handle* h, int i, size_t P, int maxb) {
     return RTG_OK;
 }
 
-static int ensure_ovf(rtg_handle* h) {
+int ensure_ovf(rtg_handle* h) {
     int grid = std::max(h->trace_blocks, h->trace_blocks_count);
     // deepest stack: one entry per BVH2 level, or up to RTG_WIDTH-1 per wide level (each wide
     // level descends at least one BVH2 level)
@@ -1259,6 +1231,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     h->cam.ox = d->camera.origin[0];
     h->cam.oy = d->camera.origin[1];
     h->cam.oz = d->camera.origin[2];
+    h->proj = d->projection;
     h->cam.width = d->camera.width;
     h->cam.height = d->camera.height;
     h->W = (int)d->camera.width;
@@ -1282,7 +1255,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_trace<true>, RTG_TB, 0));
     h->trace_blocks_count = h->n_cu * std::max(1, occ3);
     int occs = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occs, k_shade, RTG_TB, 0));
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occs, k_shade<false>, RTG_TB, 0));
     h->shade_blocks = h->n_cu * std::max(1, occs);
     return ensure_ovf(h);
 }
@@ -1318,7 +1291,7 @@ void rtg_destroy(rtg_handle* h) {
 }
 
 int rtg_set_integrator(rtg_handle* h, int integrator) {
-    if (!h || integrator < RTG_INTEGRATOR_PATH || integrator > RTG_INTEGRATOR_NORMALS) {
+    if (!h || integrator < RTG_INTEGRATOR_PATH || integrator > RTG_INTEGRATOR_DIRECT_MIS) {
         g_err = "rtg_set_integrator: bad argument";
         return RTG_ERR_ARG;
     }
@@ -1337,8 +1310,10 @@ int rtg_set_options(rtg_handle* h, int max_depth, int cull, uint32_t max_paths) 
     return RTG_OK;
 }
 
+}  // extern "C"
+
 // Pixel list in tile order (32x32 tiles, row-major inside a tile), for the requested tiles.
-static int set_pixels(rtg_handle* h, const uint32_t* tiles, uint32_t n_tiles) {
+int set_pixels(rtg_handle* h, const uint32_t* tiles, uint32_t n_tiles) {
     const int TS = 32;
     const uint32_t tx = (h->W + TS - 1) / TS, ty = (h->H + TS - 1) / TS;
     std::vector<uint32_t> key;
@@ -1359,6 +1334,9 @@ static int set_pixels(rtg_handle* h, const uint32_t* tiles, uint32_t n_tiles) {
     } else {
         for (uint32_t t = 0; t < tx * ty; ++t) add_tile(t);
     }
+    // launches already queued may still read the old list (rtg_render_async, adaptive groups):
+    // drain them before it is overwritten (hipMemcpy does not order against non-blocking streams)
+    HIPOK(hipDeviceSynchronize());
     if (pix.size() > h->cap_pix) {
         (void)hipFree(h->d_pix);
         HIPOK(hipMalloc((void**)&h->d_pix, std::max<size_t>(pix.size(), 1) * 4));
@@ -1370,14 +1348,19 @@ static int set_pixels(rtg_handle* h, const uint32_t* tiles, uint32_t n_tiles) {
     return RTG_OK;
 }
 
-#define LAUNCH_OK(name)                                                                      \
-    do {                                                                                     \
-        hipError_t e_ = hipGetLastError();                                                   \
-        if (e_ != hipSuccess) {                                                              \
-            g_err = std::string("launch ") + name + ": " + hipGetErrorString(e_);            \
-            return RTG_ERR_HIP;                                                              \
-        }                                                                                    \
-    } while (0)
+int launch_generate(rtg_handle* h, const ChunkArgs& a, const PathBufs& pb, hipStream_t st) {
+    (void)h;
+    hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, pb);
+    LAUNCH_OK("k_generate");
+    return RTG_OK;
+}
+
+int launch_trace(rtg_handle* h, const TraceIO& io, hipStream_t st) {
+    if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
+    else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
+    LAUNCH_OK("k_trace");
+    return RTG_OK;
+}
 
 static void timed_begin(rtg_handle* h, hipStream_t st, size_t k) {
     if (!h->timing) return;
@@ -1388,13 +1371,15 @@ static void timed_end(rtg_handle* h, hipStream_t st, size_t k) {
     if (h->timing) (void)hipEventRecord(h->kev[2 * k + 1], st);
 }
 
-static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed,
+int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed,
                        const uint32_t* tiles, uint32_t n_tiles, hipStream_t st) {
     int rc = set_pixels(h, tiles, n_tiles);
     if (rc) return rc;
     if (h->npix == 0 || n_samples == 0) return RTG_OK;
     if ((uint64_t)first + n_samples > 65536u) { g_err = "sample index >= 65536 (PCG stream key)"; return RTG_ERR_ARG; }
     const int maxb = h->max_depth + 2;
+    // computeDirectMIS keeps two scratch planes of per-path state in contrib planes 2 and 3
+    const int planes = h->integrator == RTG_INTEGRATOR_DIRECT_MIS ? std::max(maxb, 4) : maxb;
     uint32_t ns_chunk = std::max<uint32_t>(1, std::min<uint32_t>(n_samples, h->max_paths / std::max(1u, h->npix)));
     // Two chunk pipelines: the samples are split into (at least) two chunks that alternate between
     // the caller's stream and stream2, so that one chunk's trace drain tails (a few hundred us per
@@ -1404,7 +1389,7 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
     if (pipes == 2 && ns_chunk >= n_samples) ns_chunk = (n_samples + 1) / 2;
     const size_t P = (size_t)ns_chunk * h->npix;
     for (int i = 0; i < pipes; ++i)
-        if ((rc = ensure_chunk(h, i, P, maxb))) return rc;
+        if ((rc = ensure_chunk(h, i, P, planes))) return rc;
     if ((rc = ensure_ovf(h))) return rc;
     (void)hipGetLastError();  // drop any stale error left by other code on this thread
     HIPOK(hipEventRecord(h->ev[0], st));
@@ -1456,7 +1441,10 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
         for (int b = 0; b <= maxb; ++b) {
             if (b > 0) {
                 timed_begin(h, cs, k);
-                hipLaunchKernelGGL(k_shade, dim3(h->shade_blocks), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
+                if (h->integrator == RTG_INTEGRATOR_PATH)
+                    hipLaunchKernelGGL(k_shade<false>, dim3(h->shade_blocks), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
+                else
+                    hipLaunchKernelGGL(k_shade<true>, dim3(h->shade_blocks), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
                 LAUNCH_OK("k_shade");
                 timed_end(h, cs, k); kinds.push_back(2); ++k;
             }
@@ -1540,6 +1528,8 @@ static int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64
     return RTG_OK;
 }
 
+extern "C" {
+
 int rtg_render_async(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, const uint32_t* tiles,
                      uint32_t n_tiles, void* stream) {
     if (!h) { g_err = "null handle"; return RTG_ERR_ARG; }
@@ -1552,6 +1542,87 @@ int rtg_render(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, const u
     int rc = rtg_render_async(h, first, n, seed, tiles, n_tiles, nullptr);
     if (rc) return rc;
     return rtg_synchronize(h);
+}
+
+int rtg_render_adaptive(rtg_handle* h, uint32_t first, uint64_t seed, uint32_t init_samples, uint32_t max_samples,
+                        uint32_t min_samples, uint32_t* tile_samples) {
+    if (!h || init_samples == 0) { g_err = "rtg_render_adaptive: bad argument"; return RTG_ERR_ARG; }
+    HIPOK(hipSetDevice(h->device));
+    hipStream_t st = h->stream;
+    const size_t nf = (size_t)h->W * h->H * 3;
+    const uint32_t spp0 = h->spp;
+    const int TS = 32;
+    const uint32_t tx = (h->W + TS - 1) / TS, ty = (h->H + TS - 1) / TS, nt = tx * ty;
+    float* d_tmp = nullptr;
+    HIPOK(hipMalloc((void**)&d_tmp, nf * sizeof(float)));
+    float* d_keep = h->d_film;
+    auto fail = [&](int rc) { h->d_film = d_keep; (void)hipFree(d_tmp); h->spp = spp0; return rc; };
+    // ---- pass 1 (adaptiveSampling, Renderer.h:583-638): per-pixel sums of init_samples samples
+    h->d_film = d_tmp;
+    if (hipMemsetAsync(d_tmp, 0, nf * sizeof(float), st) != hipSuccess) return fail(RTG_ERR_HIP);
+    int rc = render_impl(h, first, init_samples, seed, nullptr, 0, st);
+    if (rc) return fail(rc);
+    std::vector<float> sums(nf);
+    if (hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(sums.data(), d_tmp, nf * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) {
+        g_err = "rtg_render_adaptive: pass-1 readback failed";
+        return fail(RTG_ERR_HIP);
+    }
+    std::vector<float> var(nt, 0.0f);
+    const float fi = (float)init_samples;
+    std::vector<float> est;
+    for (uint32_t t = 0; t < nt; ++t) {
+        const uint32_t x0 = (t % tx) * TS, y0 = (t / tx) * TS;
+        const uint32_t x1 = std::min<uint32_t>(x0 + TS, h->W), y1 = std::min<uint32_t>(y0 + TS, h->H);
+        est.clear();
+        for (uint32_t y = y0; y < y1; ++y)
+            for (uint32_t x = x0; x < x1; ++x)
+                for (int c = 0; c < 3; ++c) est.push_back(sums[((size_t)y * h->W + x) * 3 + c] / fi);
+        const int n = (int)(est.size() / 3);
+        float gt[3] = {0.0f, 0.0f, 0.0f}, sq[3] = {0.0f, 0.0f, 0.0f};
+        for (int i = 0; i < n; ++i)
+            for (int c = 0; c < 3; ++c) gt[c] = gt[c] + est[3 * i + c];
+        for (int c = 0; c < 3; ++c) gt[c] = gt[c] / (float)n;
+        for (int i = 0; i < n; ++i)
+            for (int c = 0; c < 3; ++c) {
+                const float d = est[3 * i + c] - gt[c];
+                sq[c] = sq[c] + d * d;
+            }
+        var[t] = (((sq[0] + sq[1]) + sq[2]) / 3.0f) / (float)(n - 1);
+    }
+    float total = 0.0f;
+    for (uint32_t t = 0; t < nt; ++t) total += var[t];
+    // ---- pass 2 (sampleTileWithWeight, Renderer.h:640-672): tiles grouped by sample count
+    std::vector<std::pair<uint32_t, uint32_t>> cnt(nt);  // (samples, tile)
+    for (uint32_t t = 0; t < nt; ++t) {
+        float w = (total > 0.0f) ? var[t] / total : 0.0f;
+        w = std::sqrt(w);
+        int smp = (int)(w * (float)max_samples);
+        smp = smp > (int)min_samples ? smp : (int)min_samples;
+        cnt[t] = {(uint32_t)smp, t};
+        if (tile_samples) tile_samples[t] = (uint32_t)smp;
+    }
+    std::sort(cnt.begin(), cnt.end());
+    for (size_t i = 0; i < cnt.size();) {
+        size_t j = i;
+        std::vector<uint32_t> group;
+        while (j < cnt.size() && cnt[j].first == cnt[i].first) group.push_back(cnt[j++].second);
+        const uint32_t n = cnt[i].first;
+        i = j;
+        if (n == 0) continue;
+        h->d_film = d_tmp;
+        if (hipMemsetAsync(d_tmp, 0, nf * sizeof(float), st) != hipSuccess) return fail(RTG_ERR_HIP);
+        if ((rc = render_impl(h, first + init_samples, n, seed, group.data(), (uint32_t)group.size(), st))) return fail(rc);
+        h->d_film = d_keep;
+        hipLaunchKernelGGL(k_fold_mean, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, h->d_pix, h->npix,
+                           (const float*)d_tmp, (float)n, d_keep);
+        if (hipGetLastError() != hipSuccess) { g_err = "launch k_fold_mean failed"; return fail(RTG_ERR_HIP); }
+    }
+    h->d_film = d_keep;
+    HIPOK(hipStreamSynchronize(st));
+    (void)hipFree(d_tmp);
+    h->spp = spp0 + 1;  // render(): film->incrementSPP() once per frame
+    return RTG_OK;
 }
 
 int rtg_synchronize(rtg_handle* h) {

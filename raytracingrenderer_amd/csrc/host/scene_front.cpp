@@ -267,6 +267,29 @@ static bool load_scene(const std::string& dir, const rth_load_options& o, rth_sc
     s->desc.camera.origin[2] = origin.z;
     s->desc.camera.width = (float)width;
     s->desc.camera.height = (float)height;
+    {  // projectOntoCamera state: projectionMatrix, cameraToView, viewDirection, Afilm (Scene.h:22-41)
+        rtg_camera_proj& cp = s->desc.projection;
+        std::memcpy(cp.proj, P.m, sizeof(P.m));
+        M4 Vc = V;
+        M4 c2v = Vc.inverted();
+        std::memcpy(cp.camera_to_view, c2v.m, sizeof(c2v.m));
+        // inverseProjectionMatrix.mulPointAndPerspectiveDivide(Vec3(0, 0, 1)) (Core.h:310-320)
+        const float* m = invP.m;
+        const float vx = 0.0f, vy = 0.0f, vz = 1.0f;
+        V3 v1(((vx * m[0] + vy * m[1]) + vz * m[2]) + m[3], ((vx * m[4] + vy * m[5]) + vz * m[6]) + m[7],
+              ((vx * m[8] + vy * m[9]) + vz * m[10]) + m[11]);
+        float w = ((m[12] * vx) + (m[13] * vy) + (m[14] * vz)) + m[15];
+        w = 1.0f / w;
+        V3 vd(v1.x * w, v1.y * w, v1.z * w);
+        vd = V.mul_vec(vd).normalize();
+        cp.view_direction[0] = vd.x;
+        cp.view_direction[1] = vd.y;
+        cp.view_direction[2] = vd.z;
+        const float wlens = 2.0f / P.m[5];
+        const float aspect = P.m[0] / P.m[5];
+        const float hlens = wlens * aspect;
+        cp.a_film = wlens * hlens;
+    }
     s->info.width = width;
     s->info.height = height;
 

@@ -165,7 +165,8 @@ class RayTracer:
     MAX_DEPTH = 4  # Renderer.h:20
 
     INTEGRATORS = {"path": N.RTG_INTEGRATOR_PATH, "direct": N.RTG_INTEGRATOR_DIRECT,
-                   "albedo": N.RTG_INTEGRATOR_ALBEDO, "normals": N.RTG_INTEGRATOR_NORMALS}
+                   "albedo": N.RTG_INTEGRATOR_ALBEDO, "normals": N.RTG_INTEGRATOR_NORMALS,
+                   "direct_mis": N.RTG_INTEGRATOR_DIRECT_MIS}
 
     def __init__(self, scene, device=0, max_depth=MAX_DEPTH, seed=1234, cull=True, max_paths=0, wide=True,
                  integrator="path"):
@@ -183,7 +184,8 @@ class RayTracer:
 
     def set_integrator(self, integrator):
         """Per-pixel estimator: "path" (pathTrace, default), "direct", "albedo", "normals"
-        (RayTracer::direct / albedo / viewNormals, Renderer.h:393-407, 558-582)."""
+        (RayTracer::direct / albedo / viewNormals, Renderer.h:393-407, 558-582), "direct_mis"
+        (direct() with computeDirectMIS, Renderer.h:474-557)."""
         mode = self.INTEGRATORS[integrator] if isinstance(integrator, str) else int(integrator)
         _check(self._lib.rtg_set_integrator(self._h, mode), self._lib.rtg_last_error)
         self.integrator = integrator
@@ -219,6 +221,30 @@ class RayTracer:
         else:
             rc = self._lib.rtg_render_async(self._h, first, n_samples, self.seed, tp, nt, None)
         _check(rc, self._lib.rtg_last_error)
+
+    def adaptiveRender(self, init_samples=2, max_samples=10240, min_samples=1, first_sample=None):
+        """RayTracer::adaptiveRender (Renderer.h:583-749): one frame whose per-tile sample counts
+        follow the tiles' variance after init_samples samples. Returns the per-tile counts. The frame
+        draws sample indices first_sample ... first_sample + init_samples + max(count) - 1 (default:
+        frame f starts at f * (init_samples + max_samples))."""
+        first = self.getSPP() * (init_samples + max_samples) if first_sample is None else first_sample
+        counts = np.zeros(self.tiles_x * self.tiles_y, np.uint32)
+        _check(self._lib.rtg_render_adaptive(self._h, first, self.seed, init_samples, max_samples, min_samples,
+                                             N.ptr(counts, C.c_uint32)), self._lib.rtg_last_error)
+        return counts
+
+    def lightTracer(self, n_frames=1, first_frame=None):
+        """RayTracer::lightTracer (Renderer.h:221-326): width*height light paths per frame, each
+        vertex connected to the camera and splatted (Film::SPP += 1 per frame)."""
+        first = self.getSPP() if first_frame is None else first_frame
+        _check(self._lib.rtg_render_light(self._h, first, n_frames, self.seed), self._lib.rtg_last_error)
+
+    def instantRadiosity(self, n_frames=1, n_vpl=50, first_frame=None):
+        """RayTracer::instantRadiosity (Renderer.h:82-218): n_vpl VPL paths (MAX_VPL = 50) per frame,
+        then every pixel's first hit gathers all visible VPLs (Film::SPP += 1 per frame)."""
+        first = self.getSPP() if first_frame is None else first_frame
+        _check(self._lib.rtg_render_instant_radiosity(self._h, first, n_frames, self.seed, n_vpl),
+               self._lib.rtg_last_error)
 
     def synchronize(self):
         _check(self._lib.rtg_synchronize(self._h), self._lib.rtg_last_error)

@@ -120,8 +120,36 @@ def main():
     pyref.save_hdr("/tmp/rtg_golden_film.hdr", film, 3)
     np.savez_compressed(os.path.join(GOLD, "rgbe_kat.npz"), film=film, spp=3,
                         hdr=np.frombuffer(open("/tmp/rtg_golden_film.hdr", "rb").read(), np.uint8))
+    light_fixtures()
     print("golden fixtures written to", GOLD)
 
 
+def light_fixtures():
+    """Light tracing / instant radiosity pieces from the reference's own classes: the Camera members
+    and Camera::projectOntoCamera (Scene.h:14-69) on random points, and AreaLight's emission sample
+    (samplePositionFromLight + sampleDirectionFromLight + evaluate(-wi), Lights.h:30-80) on scripted
+    draws, with the shared transcendentals (libref_rtm) so the oracle must match bit for bit.
+    -> light_kat.npz"""
+    rng = np.random.default_rng(99)
+    out = {}
+    for tag, (path, w, h) in {"cornell": (os.path.join(GOLD, "scenes", "cornell-box"), 96, 64),
+                              "mat": (os.path.join(GOLD, "scenes", "cornell-mat"), 80, 60)}.items():
+        r = pyref.RefScene(path, w, h, False, flavour="rtm")
+        pts = rng.uniform(-1.2, 1.2, (2048, 3)).astype(np.float32) + np.float32([0, 1, 0])
+        pts[:64] = rng.uniform(-50, 50, (64, 3)).astype(np.float32)  # many outside the frustum
+        proj, state = r.camera_project(pts)
+        area = [i for i, l in enumerate(r.export()["lights"].tolist()) if l >= 0]
+        draws = rng.random((256, 4)).astype(np.float32)
+        draws[:8, 2] = 0.0
+        li = np.array([area[k % len(area)] for k in range(len(draws))], np.int32)
+        emits = np.array([r.light_emit(li[k], draws[k]) for k in range(len(draws))], np.float32)
+        out.update({tag + "_pts": pts, tag + "_proj": proj, tag + "_state": state, tag + "_draws": draws,
+                    tag + "_li": li, tag + "_emit": emits})
+    np.savez_compressed(os.path.join(GOLD, "light_kat.npz"), **out)
+
+
 if __name__ == "__main__":
-    main()
+    if "--light-only" in sys.argv:
+        light_fixtures()
+    else:
+        main()

@@ -230,10 +230,11 @@ def test_bathroom_filtered_crop_depth16():
                     "bathroom_f depth 16")
 
 
-@pytest.mark.parametrize("integrator", ["direct", "albedo", "normals"])
+@pytest.mark.parametrize("integrator", ["direct", "albedo", "normals", "direct_mis"])
 def test_alternative_integrators(integrator):
-    """RayTracer::direct / albedo / viewNormals (Renderer.h:393-407, 558-582) on the mixed-material
-    scene (area + env lights, glass, mirror, two-sided Lambert stubs)."""
+    """RayTracer::direct / albedo / viewNormals (Renderer.h:393-407, 558-582) and direct() with
+    computeDirectMIS (:474-557) on the mixed-material scene (area + env lights, glass, mirror,
+    two-sided Lambert stubs)."""
     s = loadScene(os.path.join(SCENES, "cornell-mat"), width=80, height=60)
     rt = RayTracer(s, seed=7, integrator=integrator)
     rt.render(3, first_sample=0)
@@ -296,3 +297,45 @@ def test_deep_bvh_stack_overflow(tmp_path, base):
         rt = RayTracer(s, cull=cull)
         assert_bitexact(rt.trace_closest(r), o.trace_closest(r), "deep BVH closest")
         assert np.array_equal(rt.trace_visible(r), o.trace_visible(r))
+
+
+def test_adaptive_render_matches_oracle():
+    """RayTracer::adaptiveRender (Renderer.h:583-749): per-tile variance, weights and sample counts,
+    and the film of mean-of-samples splats, bit-exact against the oracle (partial tiles included)."""
+    s = loadScene(os.path.join(SCENES, "cornell-mat"), width=72, height=40)
+    rt = RayTracer(s, seed=11)
+    counts = rt.adaptiveRender(init_samples=2, max_samples=12, min_samples=1, first_sample=0)
+    film, spp = rt.film()
+    ref, ref_counts = Oracle(s, 4, "rtm").render_adaptive(first=0, seed=11, init=2, max_samples=12, min_samples=1)
+    assert spp == 1
+    assert counts.tolist() == ref_counts.tolist()
+    assert counts.max() > counts.min()  # the variance actually steers the sample counts
+    assert_bitexact(film, ref, "adaptive")
+
+
+@pytest.mark.parametrize("scene_name", ["cornell-box", "cornell-mat"])
+def test_light_tracer_matches_oracle(scene_name):
+    """RayTracer::lightTracer (Renderer.h:221-326): every camera connection splatted in (path, vertex)
+    order per pixel; device records sorted by key reproduce the sequential splat loop bit for bit."""
+    s = loadScene(os.path.join(SCENES, scene_name), width=64, height=48)
+    rt = RayTracer(s, seed=5)
+    rt.lightTracer(2, first_frame=0)
+    film, spp = rt.film()
+    ref = Oracle(s, 4, "rtm").render_light(2, first=0, seed=5)
+    assert spp == 2
+    assert (ref != 0).sum() > 100
+    assert_bitexact(film, ref, "light tracer " + scene_name)
+
+
+@pytest.mark.parametrize("scene_name", ["cornell-box", "cornell-mat"])
+def test_instant_radiosity_matches_oracle(scene_name):
+    """RayTracer::instantRadiosity (Renderer.h:82-218): VPL paths, VPL order, per-pixel visibility
+    against every VPL, bit-exact; with a small path budget the VPL batches are exercised too."""
+    s = loadScene(os.path.join(SCENES, scene_name), width=48, height=40)
+    rt = RayTracer(s, seed=9, max_paths=48 * 40 * 7)
+    rt.instantRadiosity(2, n_vpl=20, first_frame=0)
+    film, spp = rt.film()
+    ref = Oracle(s, 4, "rtm").render_instant_radiosity(2, first=0, seed=9, n_vpl=20)
+    assert spp == 2
+    assert (ref != 0).sum() > 100
+    assert_bitexact(film, ref, "instant radiosity " + scene_name)

@@ -106,3 +106,34 @@ def test_oracle_alternative_integrators_plumbing():
     dr, _ = Oracle(s, 4, "rtm", integrator=1).render(2, seed=1)
     pt, _ = Oracle(s, 4, "rtm", integrator=0).render(2, seed=1)
     assert 0 < dr.mean() < pt.mean()  # direct light only is darker than full path tracing
+
+
+LIGHT_KAT = os.path.join(GOLD, "light_kat.npz")
+
+
+@pytest.mark.parametrize("tag,scene,w,h", [("cornell", "cornell-box", 96, 64), ("mat", "cornell-mat", 80, 60)])
+def test_light_tracing_pieces_match_reference(tag, scene, w, h):
+    """The camera members light tracing needs (projectionMatrix, cameraToView, viewDirection, Afilm)
+    as librth computes them, Camera::projectOntoCamera (Scene.h:55-69) and AreaLight's emission
+    sample (Lights.h:30-80) in the oracle, against the reference's own classes (light_kat.npz)."""
+    z = np.load(LIGHT_KAT)
+    s = loadScene(os.path.join(SCENES, scene), width=w, height=h)
+    pr = s.desc.projection
+    got = np.concatenate([np.array(pr.proj[:], np.float32), np.array(pr.camera_to_view[:], np.float32),
+                          np.array(pr.view_direction[:], np.float32), np.float32([pr.a_film])])
+    np.testing.assert_array_equal(got.view(np.uint32), z[tag + "_state"].view(np.uint32))
+    o = Oracle(s, 4, "rtm")
+    np.testing.assert_array_equal(o.camera_project(z[tag + "_pts"]).view(np.uint32), z[tag + "_proj"].view(np.uint32))
+    emits = np.array([o.light_emit(li, d) for li, d in zip(z[tag + "_li"], z[tag + "_draws"])], np.float32)
+    np.testing.assert_array_equal(emits.view(np.uint32), z[tag + "_emit"].view(np.uint32))
+
+
+def test_light_tracer_and_radiosity_oracles_are_deterministic():
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=40, height=32)
+    o = Oracle(s, 4, "rtm")
+    a = o.render_light(2, seed=3)
+    b = o.render_light(1, first=1, seed=3, film=o.render_light(1, first=0, seed=3))
+    np.testing.assert_array_equal(a, b)
+    assert np.isfinite(a).all() and (a > 0).sum() > 100
+    c = o.render_instant_radiosity(1, seed=3, n_vpl=10)
+    assert np.isfinite(c).all() and (c > 0).sum() > 100
