@@ -68,6 +68,7 @@ struct ChunkArgs {
     unsigned long long seed;
     int max_depth;
     int mode;                  // RTG_INTEGRATOR_* (first-hit estimators never continue a path)
+    int pm;                    // path id order: 1 pixel-major (pid = lp * ns + sl), 0 sample-major
     DevCamera cam;
 };
 
@@ -132,7 +133,9 @@ struct rtg_handle {
     uint32_t spp = 0;
     int max_depth = 4, cull = 1, count = 0, timing = 0;
     uint32_t max_paths = 1u << 26;  // 64M paths in flight (~17 GB at depth 4 of 288 GB HBM)
-    int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0, shade_blocks = 0;
+    int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0, shade_blocks = 0, packet_blocks = 0;
+    int pixel_major = 1;  // path ids pixel-major: a wave's rays share pixels (RTG_PIXEL_MAJOR=0: sample-major)
+    int packet = 0;  // RTG_PACKET=1: camera rays by the packet walk (exact, but slower: DESIGN.md §4)
     uint32_t bvh_depth = 0;
     SceneView sv{};
     DevCamera cam{};

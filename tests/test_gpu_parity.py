@@ -339,3 +339,11 @@ def test_instant_radiosity_matches_oracle(scene_name):
     assert spp == 2
     assert (ref != 0).sum() > 100
     assert_bitexact(film, ref, "instant radiosity " + scene_name)
+
+
+def test_packet_walk_is_exact(synth20k, cornell256, monkeypatch):
+    """The experimental packet walk for camera rays (RTG_PACKET=1, k_trace_packet) gives the same
+    films bit for bit."""
+    monkeypatch.setenv("RTG_PACKET", "1")
+    for s in (synth20k, cornell256):
+        assert_bitexact(gpu_film(s, 2), Oracle(s, 4, "rtm").render(2, seed=1234, threads=8)[0], "packet walk")

@@ -25,5 +25,13 @@ for k, c in agg.items():
         for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
             if n in c:
                 print("   %-24s %.3f of wave cycles" % (n, c[n] / w))
+    if c.get("TCP_TCC_READ_REQ_sum"):
+        print("   L1->L2 read latency %.0f cycles" % (c["TCP_TCC_READ_REQ_LATENCY_sum"] / c["TCP_TCC_READ_REQ_sum"]))
+    if c.get("TCP_TCC_WRITE_REQ_sum"):
+        print("   L1->L2 write latency %.0f cycles" % (c["TCP_TCC_WRITE_REQ_LATENCY_sum"] / c["TCP_TCC_WRITE_REQ_sum"]))
+    if c.get("SQ_WAVES") and c.get("SQ_INSTS_VALU"):
+        print("   VALU instructions per wave %.0f, VMEM rd %.1f wr %.1f per wave" % (
+            c["SQ_INSTS_VALU"] / c["SQ_WAVES"], c.get("SQ_INSTS_VMEM_RD", 0) / c["SQ_WAVES"],
+            c.get("SQ_INSTS_VMEM_WR", 0) / c["SQ_WAVES"]))
     if c.get("TCC_HIT_sum"):
         print("   L2 hit rate %.3f" % (c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"])))
