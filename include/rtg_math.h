@@ -89,6 +89,26 @@ RTM_FN double rtm_sincos_d(double x, int want_cos)
     return v;
 }
 
+/* sin and cos of one argument: one reduction, both kernels, then branch-free quadrant selects (no
+ * lane divergence on the GPU). Bit-identical to rtm_sincos_d(x, 0) and rtm_sincos_d(x, 1): the same
+ * operations on the same operands; only the choice of result is a select instead of a switch. */
+RTM_FN void rtm_sincos2_d(double x, double* sn, double* cs)
+{
+    if (rtm_isnan_d(x) || rtm_fabs_d(x) > 1.0e300) { *sn = x - x; *cs = x - x; return; }
+    if (x == 0.0) { *sn = x; *cs = 1.0; return; }
+    double fk = x * RTM_INV_PIO2;
+    int k = (int)(fk + (fk >= 0.0 ? 0.5 : -0.5));
+    double dk = (double)k;
+    double r = (x - dk * RTM_PIO2_HI) - dk * RTM_PIO2_LO;
+    double s = rtm_ksin(r), c = rtm_kcos(r);
+    int q = k & 3;
+    /* sin: q = 0 s, 1 c, 2 -s, 3 -c;  cos = sin at quadrant q + 1 */
+    double a = (q & 1) ? c : s;
+    double b = (q & 1) ? s : c;
+    *sn = (q & 2) ? -a : a;
+    *cs = ((q + 1) & 2) ? -b : b;
+}
+
 /* atan for 0 <= t <= 1: nearest node c = j/8, atan(t) = atan(c) + atan((t-c)/(1+t*c)). */
 RTM_FN double rtm_atan01(double t)
 {
@@ -131,7 +151,11 @@ RTM_FN double rtm_atan2_d(double y, double x)
         else if (ax == big) r = xs ? RTM_PI : 0.0;
         else r = RTM_PI_2;
     } else {
-        double base = (ay <= ax) ? rtm_atan01(ay / ax) : RTM_PI_2 - rtm_atan01(ax / ay);
+        /* (ay <= ax) ? atan01(ay / ax) : pi/2 - atan01(ax / ay), with one division and one
+         * atan01 (operand selects instead of two divergent branches) */
+        int lo = ay <= ax;
+        double at = rtm_atan01((lo ? ay : ax) / (lo ? ax : ay));
+        double base = lo ? at : RTM_PI_2 - at;
         r = xs ? RTM_PI - base : base;
     }
     return ys ? -r : r;
@@ -160,6 +184,13 @@ RTM_FN double rtm_acos_d(double x)
 /* ---- float API (drop-in for the libm calls on the reference hot path) ---- */
 RTM_FN float rtm_sinf(float x) { return (float)rtm_sincos_d((double)x, 0); }
 RTM_FN float rtm_cosf(float x) { return (float)rtm_sincos_d((double)x, 1); }
+RTM_FN void rtm_sincosf(float x, float* sn, float* cs)
+{
+    double s, c;
+    rtm_sincos2_d((double)x, &s, &c);
+    *sn = (float)s;
+    *cs = (float)c;
+}
 RTM_FN float rtm_acosf(float x) { return (float)rtm_acos_d((double)x); }
 RTM_FN float rtm_atan2f(float y, float x) { return (float)rtm_atan2_d((double)y, (double)x); }
 

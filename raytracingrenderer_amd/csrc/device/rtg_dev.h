@@ -18,6 +18,7 @@
 #ifdef RTG_TIMING_ONLY_FAST_MATH  // A/B experiment only: NOT bit-faithful, never shipped
 #define rtm_sinf(x) __sinf(x)
 #define rtm_cosf(x) __cosf(x)
+#define rtm_sincosf(x, s, c) __sincosf(x, s, c)
 #define rtm_acosf(x) acosf(x)
 #define rtm_atan2f(y, x) atan2f(y, x)
 #endif
@@ -224,7 +225,10 @@ RTG_D v3 tex_sample(const SceneView& s, int tex, float tu, float tv) {
 
 // ------------------------------------------------------------------ sampling (Sampling.h)
 RTG_D v3 spherical_to_world(float theta, float phi) {  // Core.h:547-550
-    return mk(rtm_cosf(phi) * rtm_sinf(theta), rtm_sinf(phi) * rtm_sinf(theta), rtm_cosf(theta));
+    float st, ct, sp, cp;  // rtm_sincosf: bit-identical to rtm_sinf / rtm_cosf
+    rtm_sincosf(theta, &st, &ct);
+    rtm_sincosf(phi, &sp, &cp);
+    return mk(cp * st, sp * st, ct);
 }
 RTG_D v3 cosine_sample_hemisphere(float r1, float r2) {
     float theta = rtm_acosf(sqrtf(r1));

@@ -31,11 +31,33 @@ using namespace rtgd;
 #define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel
 #endif
 #define RTG_CULL_REL 1.52587890625e-05f  // 2^-16 relative inflation for distance culling
+#ifndef RTG_FETCH
+#define RTG_FETCH 256       // rays a wave takes from the work counter per atomic (k_trace pool; 64: -3.5 %)
+#endif
+#ifndef RTG_SHADE_BUF
+#define RTG_SHADE_BUF 0     // >0: k_shade stages compacted path ids in LDS (entries per queue) and
+                            // appends them with one atomic per flush instead of one per 256 paths
+#endif
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 4                // min waves per SIMD for k_shade (register budget)
 #endif
 
-struct __align__(16) Counters { unsigned n_ext, n_shadow, f_ext, f_shadow, f_shade, pad0, pad1, pad2; };
+// Work counters of one bounce. Every field sits in its own 128-B line (RTG_CTR_PAD): the
+// device-scope atomics on them (queue appends in k_shade, work fetches in k_trace) are served one
+// line at a time, so counters sharing a line serialise with each other.
+#ifndef RTG_CTR_PAD
+#define RTG_CTR_PAD 1
+#endif
+#if RTG_CTR_PAD
+#define RTG_CPAD(f) unsigned f; unsigned f##_pad[31];
+#else
+#define RTG_CPAD(f) unsigned f;
+#endif
+struct __align__(16) Counters {
+    RTG_CPAD(n_ext) RTG_CPAD(n_shadow) RTG_CPAD(f_ext) RTG_CPAD(f_shadow) RTG_CPAD(f_shade) RTG_CPAD(pad0)
+    RTG_CPAD(pad1) RTG_CPAD(pad2)
+};
+#undef RTG_CPAD
 
 // Queues hold path ids only; ray payloads live in per-path arrays (written in place by k_shade),
 // so compaction moves 4 bytes per ray and needs one atomic per 256 paths.

@@ -77,14 +77,14 @@ void k_trace(SceneView s, TraceIO io) {
         if (im != 0 && !drained && (__popcll(im) >= RTG_REFILL || __ballot(have) == 0)) {
             if (pool_left == 0) {
                 unsigned b = 0;
-                if (lane == 0) b = atomicAdd(io.fetch, 64u);
+                if (lane == 0) b = atomicAdd(io.fetch, (unsigned)RTG_FETCH);
                 b = __shfl(b, 0);
                 if (b >= n) {
                     drained = true;
                     if (io.wtime && lane == 0) io.wtime[3 * wslot + 1] = __builtin_amdgcn_s_memrealtime();
                 } else {
                     pool_base = b;
-                    pool_left = min(64u, n - b);
+                    pool_left = min((unsigned)RTG_FETCH, n - b);
                 }
             }
             if (pool_left > 0) {
@@ -637,6 +637,10 @@ template <bool ALT>
 __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
     __shared__ unsigned s_cnt[2][RTG_TB / 64];
     __shared__ unsigned s_base[2];
+#if RTG_SHADE_BUF
+    __shared__ unsigned s_q[2][RTG_SHADE_BUF];
+    unsigned fill_e = 0, fill_s = 0;  // block-uniform fill of the LDS id buffers
+#endif
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     const unsigned n = p.ctr[b].n_ext;
@@ -885,6 +889,48 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             s_cnt[1][wave] = (unsigned)__popcll(ms);
         }
         __syncthreads();
+#if RTG_SHADE_BUF
+        {
+            // stage the ids in LDS; append a buffer to its queue (one atomic) once another
+            // iteration might not fit, and at the block's last iteration
+            unsigned oe = fill_e, os = fill_s, te = 0, ts = 0;
+            for (int w = 0; w < RTG_TB / 64; ++w) {
+                if (w < wave) {
+                    oe += s_cnt[0][w];
+                    os += s_cnt[1][w];
+                }
+                te += s_cnt[0][w];
+                ts += s_cnt[1][w];
+            }
+            if (want_ext) s_q[0][oe + prefix_lt(me)] = (unsigned)pid;
+            if (want_sh) s_q[1][os + prefix_lt(ms)] = (unsigned)pid;
+            fill_e += te;
+            fill_s += ts;
+            const bool last = base + gridDim.x * RTG_TB >= n;
+            const bool fe = fill_e > RTG_SHADE_BUF - RTG_TB || (last && fill_e);
+            const bool fs = fill_s > RTG_SHADE_BUF - RTG_TB || (last && fill_s);
+            __syncthreads();
+            if (fe || fs) {
+                if (threadIdx.x == 0) {
+                    s_base[0] = fe ? atomicAdd(&p.ctr[b + 1].n_ext, fill_e) : 0u;
+                    s_base[1] = fs ? atomicAdd(&p.ctr[b].n_shadow, fill_s) : 0u;
+                }
+                __syncthreads();
+                if (fe) {
+                    const unsigned ob = s_base[0];
+                    for (unsigned j = threadIdx.x; j < fill_e; j += RTG_TB) qout[ob + j] = s_q[0][j];
+                    fill_e = 0;
+                }
+                if (fs) {
+                    const unsigned ob = s_base[1];
+                    for (unsigned j = threadIdx.x; j < fill_s; j += RTG_TB) p.shq[ob + j] = s_q[1][j];
+                    fill_s = 0;
+                }
+                __syncthreads();
+            }
+            continue;
+        }
+#endif
         if (threadIdx.x == 0) {
             unsigned te = 0, ts = 0;
             for (int w = 0; w < RTG_TB / 64; ++w) {

@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 mkdir -p raytracingrenderer_amd/lib/ab
 while [ $# -ge 2 ]; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -shared $2 \
-    -o raytracingrenderer_amd/lib/ab/$1.so raytracingrenderer_amd/csrc/device/rtg_kernels.hip &
+    -o raytracingrenderer_amd/lib/ab/$1.so raytracingrenderer_amd/csrc/device/rtg_kernels.hip raytracingrenderer_amd/csrc/device/rtg_light.hip &
   shift 2
 done
 wait
