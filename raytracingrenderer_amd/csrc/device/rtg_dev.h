@@ -211,9 +211,11 @@ RTG_D v3 bilinear(const float* T, int w, int h, float tu, float tv) {
     float w1 = fu * (1.0f - fv);
     float w2 = (1.0f - fu) * fv;
     float w3 = fu * fv;
-    x = x % w;
-    y = y % h;
-    int x1 = (x + 1) % w, y1 = (y + 1) % h;
+    // x, y >= 0 here (u, v are >= 0 or +inf), so the modulo runs only when the coordinate wraps
+    // and (x + 1) % w is a compare: same values as the reference's x % w, (x + 1) % w
+    x = x < w ? x : x % w;
+    y = y < h ? y : y % h;
+    const int x1 = (x + 1 == w) ? 0 : x + 1, y1 = (y + 1 == h) ? 0 : y + 1;
     v3 s0 = texel(T, y * w + x), s1 = texel(T, y * w + x1);
     v3 s2 = texel(T, y1 * w + x), s3 = texel(T, y1 * w + x1);
     return add(add(add(muls(s0, w0), muls(s1, w1)), muls(s2, w2)), muls(s3, w3));

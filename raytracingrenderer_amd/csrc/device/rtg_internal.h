@@ -38,6 +38,9 @@ using namespace rtgd;
 #define RTG_SHADE_BUF 0     // >0: k_shade stages compacted path ids in LDS (entries per queue) and
                             // appends them with one atomic per flush instead of one per 256 paths
 #endif
+#ifndef RTG_SHADE_SORT
+#define RTG_SHADE_SORT 0    // 1: k_shade partitions each block's paths into misses and hits first (C3: no change)
+#endif
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 4                // min waves per SIMD for k_shade (register budget)
 #endif

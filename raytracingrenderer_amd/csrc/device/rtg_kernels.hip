@@ -637,6 +637,9 @@ template <bool ALT>
 __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
     __shared__ unsigned s_cnt[2][RTG_TB / 64];
     __shared__ unsigned s_base[2];
+#if RTG_SHADE_SORT
+    __shared__ int s_sort[RTG_TB];
+#endif
 #if RTG_SHADE_BUF
     __shared__ unsigned s_q[2][RTG_SHADE_BUF];
     unsigned fill_e = 0, fill_s = 0;  // block-uniform fill of the LDS id buffers
@@ -652,8 +655,40 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
         const unsigned i = base + threadIdx.x;
         int pid = 0;
         bool want_ext = false, want_sh = false;
-        if (i < n) {
+        bool valid = i < n;
+#if RTG_SHADE_SORT
+        {
+            // stable block-level partition of the 256 path ids: misses first, then hits, so that
+            // waves run the miss branch (background lookup) and the surface branch without lane
+            // divergence between them (at most one wave holds both)
+            const int p0 = valid ? (int)qin[i] : 0;
+            const bool miss = valid && !(p.hits[p0].x < RTG_FLT_MAX);
+            const unsigned long long mm = __ballot(miss), mh = __ballot(valid && !miss);
+            if (lane == 0) {
+                s_cnt[0][wave] = (unsigned)__popcll(mm);
+                s_cnt[1][wave] = (unsigned)__popcll(mh);
+            }
+            __syncthreads();
+            unsigned nm = 0, om = 0, oh = 0, nv = 0;
+            for (int w = 0; w < RTG_TB / 64; ++w) {
+                if (w < wave) {
+                    om += s_cnt[0][w];
+                    oh += s_cnt[1][w];
+                }
+                nm += s_cnt[0][w];
+                nv += s_cnt[0][w] + s_cnt[1][w];
+            }
+            if (miss) s_sort[om + prefix_lt(mm)] = p0;
+            else if (valid) s_sort[nm + oh + prefix_lt(mh)] = p0;
+            __syncthreads();
+            valid = threadIdx.x < nv;
+            pid = valid ? s_sort[threadIdx.x] : 0;
+        }
+#endif
+        if (valid) {
+#if !RTG_SHADE_SORT
             pid = (int)qin[i];
+#endif
             const float4 ro = p.ray_o[pid], rd = p.ray_d[pid];
             const float4 h = p.hits[pid];
             const v3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
@@ -973,6 +1008,42 @@ __global__ __launch_bounds__(RTG_TB) void k_accumulate(ChunkArgs a, PathBufs p, 
     film[(size_t)pixel * 3 + 0] = fr;
     film[(size_t)pixel * 3 + 1] = fg;
     film[(size_t)pixel * 3 + 2] = fb;
+}
+
+// Pixel-major chunks (pid = lp * ns + sl): one wave per pixel, lane = sample, so the contrib reads
+// are contiguous. Each lane folds its path's right-nested sum; then lanes 0-2 (R, G, B) add the
+// samples to the film in sample order from LDS: the same additions in the same order as
+// k_accumulate, so the same bits.
+__global__ __launch_bounds__(RTG_TB) void k_accumulate_pm(ChunkArgs a, PathBufs p, float* film) {
+    __shared__ float s_acc[RTG_TB / 64][64][4];
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    const unsigned lp = blockIdx.x * (RTG_TB / 64) + wave;
+    const bool active = lp < a.npix;  // wave-uniform
+    const unsigned pixel = active ? a.pixlist[lp] : 0u;
+    float fc = (active && lane < 3) ? film[(size_t)pixel * 3 + lane] : 0.0f;
+    for (unsigned s0 = 0; s0 < a.ns; s0 += 64) {
+        const unsigned sl = s0 + lane;
+        float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (active && sl < a.ns) {
+            const unsigned pid = lp * a.ns + sl;
+            const int nt = p.meta[pid] & 0xff;
+            acc = p.contrib[(size_t)(nt - 1) * a.P + pid];
+            for (int j = nt - 2; j >= 0; --j) {
+                const float4 c = p.contrib[(size_t)j * a.P + pid];
+                acc = make_float4(c.x + acc.x, c.y + acc.y, c.z + acc.z, 0.0f);
+            }
+        }
+        s_acc[wave][lane][0] = acc.x;
+        s_acc[wave][lane][1] = acc.y;
+        s_acc[wave][lane][2] = acc.z;
+        __syncthreads();
+        const unsigned cnt = min(64u, a.ns - s0);
+        if (active && lane < 3)
+            for (unsigned j = 0; j < cnt; ++j) fc = fc + s_acc[wave][j][lane];
+        __syncthreads();
+    }
+    if (active && lane < 3) film[(size_t)pixel * 3 + lane] = fc;
 }
 
 // sampleTileWithWeight's splat (Renderer.h:661-670): film += (sum of n samples) / (float)n for the
@@ -1720,7 +1791,11 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         LAUNCH_OK("k_tally");
         if (pipes == 2 && c > 0) HIPOK(hipStreamWaitEvent(cs, h->pev[3], 0));  // fold order
         timed_begin(h, cs, k);
-        hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, cs, a, pb, h->d_film);
+        if (a.pm && a.ns > 1)
+            hipLaunchKernelGGL(k_accumulate_pm, dim3((h->npix + RTG_TB / 64 - 1) / (RTG_TB / 64)), dim3(RTG_TB), 0, cs, a,
+                               pb, h->d_film);
+        else
+            hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, cs, a, pb, h->d_film);
         LAUNCH_OK("k_accumulate");
         timed_end(h, cs, k); kinds.push_back(2); ++k;
         if (pipes == 2) HIPOK(hipEventRecord(h->pev[3], cs));
