@@ -125,6 +125,8 @@ def main():
         rt.render(a.spp, tiles=tiles, first_sample=0)
         if world > 1:
             if backend == "nccl":
+                import torch
+                torch.cuda.synchronize()  # the previous step's reduce is done with film_t
                 rt.copy_film_to(film_t.data_ptr())
             else:
                 film_t.copy_(torch.from_numpy(rt.film()[0]))

@@ -34,9 +34,21 @@ using namespace rtgd;
 #ifndef RTG_FETCH
 #define RTG_FETCH 256       // rays a wave takes from the work counter per atomic (k_trace pool; 64: -3.5 %)
 #endif
+#ifndef RTG_FETCH_TAIL
+#define RTG_FETCH_TAIL 4    // k: fetch 64 rays per atomic once about k rounds of big batches are left
+#endif
+#ifndef RTG_FETCH_ADAPT
+#define RTG_FETCH_ADAPT 0   // 1: big batch = min(RTG_FETCH, ~1/16 of a wave's share) (no gain)
+#endif
 #ifndef RTG_SHADE_BUF
 #define RTG_SHADE_BUF 0     // >0: k_shade stages compacted path ids in LDS (entries per queue) and
                             // appends them with one atomic per flush instead of one per 256 paths
+#endif
+#ifndef RTG_FAST_PUSH
+#define RTG_FAST_PUSH 1     // wide-node pushes as three unconditional LDS writes when they fit (~1 %)
+#endif
+#ifndef RTG_SEL_SORT
+#define RTG_SEL_SORT 0      // 1: slot sort network as selects instead of branches
 #endif
 #ifndef RTG_SHADE_SORT
 #define RTG_SHADE_SORT 0    // 1: k_shade partitions each block's paths into misses and hits first (C3: no change)

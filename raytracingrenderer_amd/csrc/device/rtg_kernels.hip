@@ -51,7 +51,11 @@ void k_trace(SceneView s, TraceIO io) {
     const unsigned n = nc + (io.scount ? *io.scount : 0u);
     unsigned long long c_nodes = 0, c_tris = 0, c_snodes = 0, c_stris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0,
                        c_cullpop = 0, c_pops = 0, c_lslots = 0;
-    unsigned pool_base = 0, pool_left = 0;  // wave-uniform
+    unsigned pool_base = 0, pool_left = 0, last_b = 0;  // wave-uniform
+    // batch size: RTG_FETCH, or (RTG_FETCH_ADAPT) about 1/16 of a wave's share of this launch
+    const unsigned fetch_big = RTG_FETCH_ADAPT ? min((unsigned)RTG_FETCH, max(64u, n / (gthreads / 64u) / 16u))
+                                               : (unsigned)RTG_FETCH;
+    const unsigned tail_rays = (gthreads / 64u) * fetch_big * RTG_FETCH_TAIL;
     bool drained = false;                   // wave-uniform
     bool have = false;
     unsigned ri = 0;
@@ -77,14 +81,18 @@ void k_trace(SceneView s, TraceIO io) {
         if (im != 0 && !drained && (__popcll(im) >= RTG_REFILL || __ballot(have) == 0)) {
             if (pool_left == 0) {
                 unsigned b = 0;
-                if (lane == 0) b = atomicAdd(io.fetch, (unsigned)RTG_FETCH);
+                // big batches (one atomic per RTG_FETCH rays) until about one round of them is
+                // left, judged from this wave's previous fetch, then 64 (shorter drain tails)
+                const unsigned g = (RTG_FETCH_TAIL && last_b + tail_rays >= n) ? 64u : fetch_big;
+                if (lane == 0) b = atomicAdd(io.fetch, g);
                 b = __shfl(b, 0);
+                last_b = b;
                 if (b >= n) {
                     drained = true;
                     if (io.wtime && lane == 0) io.wtime[3 * wslot + 1] = __builtin_amdgcn_s_memrealtime();
                 } else {
                     pool_base = b;
-                    pool_left = min((unsigned)RTG_FETCH, n - b);
+                    pool_left = min(g, n - b);
                 }
             }
             if (pool_left > 0) {
@@ -293,11 +301,22 @@ void k_trace(SceneView s, TraceIO io) {
             }
 #endif
             // ascending entry distance (misses sort last); order only affects culling, not results
+#if RTG_SEL_SORT  // compare-exchange as selects (v_cndmask), no exec-mask branches
+#define RTG_CSWAP(i, j)                                                          \
+    {                                                                           \
+        const bool sw = key[j] < key[i];                                        \
+        const float ki = key[i], kj = key[j];                                   \
+        const int wi = wd[i], wj = wd[j];                                       \
+        key[i] = sw ? kj : ki; key[j] = sw ? ki : kj;                           \
+        wd[i] = sw ? wj : wi; wd[j] = sw ? wi : wj;                             \
+    }
+#else
 #define RTG_CSWAP(i, j)                                               \
     if (key[j] < key[i]) {                                           \
         const float tk = key[i]; key[i] = key[j]; key[j] = tk;      \
         const int tw = wd[i]; wd[i] = wd[j]; wd[j] = tw;             \
     }
+#endif
 #if RTG_WIDTH == 4
             RTG_CSWAP(0, 1) RTG_CSWAP(2, 3) RTG_CSWAP(0, 2) RTG_CSWAP(1, 3) RTG_CSWAP(1, 2)
 #else
@@ -312,6 +331,17 @@ void k_trace(SceneView s, TraceIO io) {
             // misses carry +inf and sort last
             if (key[0] == __builtin_inff()) {
                 cur = RTG_POP;
+#if RTG_FAST_PUSH && RTG_WIDTH == 4
+            } else if (!COUNT && sp + 3 <= RTG_STACK) {
+                // hits are a prefix of the sorted slots: push the h = hits - 1 far ones (far first)
+                // with three unconditional LDS writes; entries above sp + h are never read
+                const int h = (key[1] != __builtin_inff()) + (key[2] != __builtin_inff()) + (key[3] != __builtin_inff());
+                stk[sp][tid] = h == 3 ? wd[3] : (h == 2 ? wd[2] : wd[1]);
+                stk[sp + 1][tid] = h == 3 ? wd[2] : wd[1];
+                stk[sp + 2][tid] = wd[1];
+                sp += h;
+                cur = wd[0];
+#endif
             } else {
 #pragma unroll
                 for (int k = RTG_WIDTH - 1; k >= 1; --k) {
