@@ -44,6 +44,8 @@ def lib(flavour="rtm"):
             getattr(L, fn).argtypes = [C.c_float]
         L.or_atan2f.restype = C.c_float
         L.or_atan2f.argtypes = [C.c_float, C.c_float]
+        L.or_sincos_mismatch.restype = C.c_long
+        L.or_sincos_mismatch.argtypes = [f32p, C.c_long]
         _libs[flavour] = L
     return _libs[flavour]
 

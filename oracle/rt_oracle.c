@@ -1104,3 +1104,15 @@ float or_acosf(float x) { return O_ACOSF(x); }
 float or_sinf(float x) { return O_SINF(x); }
 float or_cosf(float x) { return O_COSF(x); }
 float or_atan2f(float y, float x) { return O_ATAN2F(y, x); }
+/* rtm_sincosf (the GPU's fused form) against rtm_sinf / rtm_cosf on n inputs: number of inputs
+ * whose bits differ in either result. */
+long or_sincos_mismatch(const float* x, long n)
+{
+    long bad = 0;
+    for (long i = 0; i < n; ++i) {
+        float s, c, s1 = rtm_sinf(x[i]), c1 = rtm_cosf(x[i]);
+        rtm_sincosf(x[i], &s, &c);
+        if (memcmp(&s, &s1, 4) != 0 || memcmp(&c, &c1, 4) != 0) ++bad;
+    }
+    return bad;
+}

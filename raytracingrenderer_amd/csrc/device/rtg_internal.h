@@ -35,7 +35,10 @@ using namespace rtgd;
 #define RTG_FETCH 256       // rays a wave takes from the work counter per atomic (k_trace pool; 64: -3.5 %)
 #endif
 #ifndef RTG_FETCH_TAIL
-#define RTG_FETCH_TAIL 4    // k: fetch 64 rays per atomic once about k rounds of big batches are left
+#define RTG_FETCH_TAIL 8    // k: fetch 64 rays per atomic once about k rounds of big batches are left
+#endif
+#ifndef RTG_FETCH8
+#define RTG_FETCH8 1        // k_trace fetches from 8 slice counters (TraceIO::fetch8): +4 % per GPU at N=8
 #endif
 #ifndef RTG_FETCH_ADAPT
 #define RTG_FETCH_ADAPT 0   // 1: big batch = min(RTG_FETCH, ~1/16 of a wave's share) (no gain)
@@ -71,6 +74,7 @@ using namespace rtgd;
 struct __align__(16) Counters {
     RTG_CPAD(n_ext) RTG_CPAD(n_shadow) RTG_CPAD(f_ext) RTG_CPAD(f_shadow) RTG_CPAD(f_shade) RTG_CPAD(pad0)
     RTG_CPAD(pad1) RTG_CPAD(pad2)
+    unsigned f8[8 * 32];  // sliced work counters of k_trace (TraceIO::fetch8), one 128-B line each
 };
 #undef RTG_CPAD
 
@@ -92,6 +96,7 @@ struct TraceIO {
     float4* contrib;           // any-hit: this bounce's contribution plane [pid]
     int* visible;              // any-hit query output [pid] (instead of contrib)
     unsigned* fetch;           // work counter over both sets (device, zeroed)
+    unsigned* fetch8;          // or (non-null) 8 slice counters at a stride of 32 (device, zeroed)
     int* ovf;                  // global stack overflow [level][thread]
     unsigned long long* stats; // [0,1] closest / [4,5] any-hit: box tests, triangle tests (COUNT)
     int cull;
@@ -171,6 +176,7 @@ struct rtg_handle {
     int max_depth = 4, cull = 1, count = 0, timing = 0;
     uint32_t max_paths = 1u << 26;  // 64M paths in flight (~17 GB at depth 4 of 288 GB HBM)
     int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0, shade_blocks = 0, packet_blocks = 0;
+    int fetch8 = RTG_FETCH8;  // sliced work counters for k_trace (RTG_FETCH8 env overrides)
     int pixel_major = 1;  // path ids pixel-major: a wave's rays share pixels (RTG_PIXEL_MAJOR=0: sample-major)
     int packet = 0;  // RTG_PACKET=1: camera rays by the packet walk (exact, but slower: DESIGN.md §4)
     uint32_t bvh_depth = 0;

@@ -55,7 +55,10 @@ void k_trace(SceneView s, TraceIO io) {
     // batch size: RTG_FETCH, or (RTG_FETCH_ADAPT) about 1/16 of a wave's share of this launch
     const unsigned fetch_big = RTG_FETCH_ADAPT ? min((unsigned)RTG_FETCH, max(64u, n / (gthreads / 64u) / 16u))
                                                : (unsigned)RTG_FETCH;
-    const unsigned tail_rays = (gthreads / 64u) * fetch_big * RTG_FETCH_TAIL;
+    const unsigned tail_rays = (gthreads / 64u) * fetch_big * RTG_FETCH_TAIL / (io.fetch8 ? 8u : 1u);
+    auto slice_lo = [&](int k) { return io.fetch8 ? (unsigned)(((unsigned long long)n * (unsigned)k) >> 3) : 0u; };
+    int slice = io.fetch8 ? (int)(blockIdx.x & 7u) : 0, tried = 0;  // wave-uniform
+    unsigned s_lo = slice_lo(slice), s_len = (io.fetch8 ? slice_lo(slice + 1) : n) - s_lo;
     bool drained = false;                   // wave-uniform
     bool have = false;
     unsigned ri = 0;
@@ -79,20 +82,30 @@ void k_trace(SceneView s, TraceIO io) {
         // ---- refill idle lanes from the wave's pool
         const unsigned long long im = __ballot(!have);
         if (im != 0 && !drained && (__popcll(im) >= RTG_REFILL || __ballot(have) == 0)) {
-            if (pool_left == 0) {
+            // wave-uniform fetch: big batches (one atomic per fetch_big rays) until about
+            // RTG_FETCH_TAIL rounds of them are left in the slice, judged from this wave's previous
+            // fetch, then 64 (shorter drain tails). With io.fetch8 the index space is cut into 8
+            // slices with a counter each (the atomics of one counter serialise); a wave starts on
+            // slice blockIdx % 8 and moves on to the next slice when its own runs dry.
+            while (pool_left == 0) {
+                const bool tail = RTG_FETCH_TAIL && last_b + tail_rays >= s_len;
+                const unsigned g = tail ? 64u : fetch_big;
                 unsigned b = 0;
-                // big batches (one atomic per RTG_FETCH rays) until about one round of them is
-                // left, judged from this wave's previous fetch, then 64 (shorter drain tails)
-                const unsigned g = (RTG_FETCH_TAIL && last_b + tail_rays >= n) ? 64u : fetch_big;
-                if (lane == 0) b = atomicAdd(io.fetch, g);
+                if (lane == 0) b = atomicAdd(io.fetch8 ? io.fetch8 + 32 * slice : io.fetch, g);
                 b = __shfl(b, 0);
                 last_b = b;
-                if (b >= n) {
+                if (b < s_len) {
+                    pool_base = s_lo + b;
+                    pool_left = min(g, s_len - b);
+                } else if (!io.fetch8 || ++tried == 8) {
                     drained = true;
                     if (io.wtime && lane == 0) io.wtime[3 * wslot + 1] = __builtin_amdgcn_s_memrealtime();
+                    break;
                 } else {
-                    pool_base = b;
-                    pool_left = min(g, n - b);
+                    slice = (slice + 1) & 7;
+                    s_lo = slice_lo(slice);
+                    s_len = slice_lo(slice + 1) - s_lo;
+                    last_b = s_len;  // a stolen slice is near its end: small batches
                 }
             }
             if (pool_left > 0) {
@@ -1582,6 +1595,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     h->packet_blocks = h->n_cu * std::max(1, occp);
     if (const char* e = std::getenv("RTG_PACKET")) h->packet = std::atoi(e);
     if (const char* e = std::getenv("RTG_PIXEL_MAJOR")) h->pixel_major = std::atoi(e);
+    if (const char* e = std::getenv("RTG_FETCH8")) h->fetch8 = std::atoi(e);
     int occs = 0;
     HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occs, k_shade<false>, RTG_TB, 0));
     h->shade_blocks = h->n_cu * std::max(1, occs);
@@ -1794,6 +1808,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             io.contrib = b > 0 ? pb.contrib + (size_t)(b - 1) * a.P : nullptr;
             io.visible = nullptr;
             io.fetch = &pb.ctr[b].f_ext;
+            io.fetch8 = h->fetch8 ? pb.ctr[b].f8 : nullptr;
             io.wtime = (d_wt && c == 0) ? d_wt + (size_t)b * wt_waves * 3 : nullptr;
             timed_begin(h, cs, k);
             if (b == 0 && use_packet) {
@@ -1807,6 +1822,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                 lo.queue = pb.shq;
                 lo.count = &pb.ctr[0].pad0;
                 lo.fetch = &pb.ctr[0].pad1;
+                lo.fetch8 = nullptr;
                 hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, cs, h->sv, lo);
             } else if (h->count) {
                 hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, cs, h->sv, io);

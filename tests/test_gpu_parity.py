@@ -347,3 +347,14 @@ def test_packet_walk_is_exact(synth20k, cornell256, monkeypatch):
     monkeypatch.setenv("RTG_PACKET", "1")
     for s in (synth20k, cornell256):
         assert_bitexact(gpu_film(s, 2), Oracle(s, 4, "rtm").render(2, seed=1234, threads=8)[0], "packet walk")
+
+
+def test_many_samples_per_chunk_and_path_order(monkeypatch):
+    """130 samples of every pixel in one chunk: pixel-major path ids fold the film in two passes of
+    64 samples (k_accumulate_pm) and must equal the oracle bit for bit; the sample-major order
+    (RTG_PIXEL_MAJOR=0, k_accumulate) gives the same film."""
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=32, height=32)
+    ref, _ = Oracle(s, 4, "rtm").render(130, seed=1234, threads=8)
+    assert_bitexact(gpu_film(s, 130), ref, "pixel-major 130 spp")
+    monkeypatch.setenv("RTG_PIXEL_MAJOR", "0")
+    assert_bitexact(gpu_film(s, 130), ref, "sample-major 130 spp")

@@ -44,3 +44,18 @@ def test_acos_domain():
     assert np.isnan(L.or_acosf(1.0000001)) and np.isnan(L.or_acosf(float("nan")))
     assert L.or_acosf(1.0) == 0.0 and L.or_acosf(-1.0) == np.float32(np.pi)
     assert np.float32(L.or_sinf(-0.0)).tobytes() == np.float32(-0.0).tobytes()
+
+
+def test_fused_sincos_is_bit_identical():
+    """rtm_sincosf (one reduction, branch-free quadrant selects; what the device's
+    spherical_to_world uses) returns the bits of rtm_sinf / rtm_cosf."""
+    L = lib("rtm")
+    rng = np.random.default_rng(2)
+    x = np.concatenate([
+        (rng.random(2_000_000) * 2 * np.pi).astype(np.float32),            # phi = 2 pi r2
+        np.arccos(rng.random(1_000_000)).astype(np.float32),               # theta
+        rng.normal(scale=50.0, size=500_000).astype(np.float32),
+        np.array([0.0, -0.0, np.pi / 4, -np.pi / 4, 3 * np.pi / 4, np.inf, -np.inf, np.nan], np.float32),
+    ])
+    x = np.ascontiguousarray(x)
+    assert L.or_sincos_mismatch(x.ctypes.data_as(C.POINTER(C.c_float)), len(x)) == 0
