@@ -187,7 +187,7 @@ struct SceneView {
     const DevMat* mats;
     const DevLight* lights;
     const DevTex* texinfo;
-    const float* texels;
+    const float4* texels;  // RGB + pad per texel
     int n_lights;
     int env_tex;         // -1: BackgroundColour(0)
     int root_word;       // child word of the root (RTG_EXIT if no triangles)
@@ -198,8 +198,17 @@ struct SceneView {
 };
 
 // ------------------------------------------------------------------ Texture::sample
-RTG_D v3 texel(const float* t, int i) { return mk(t[i * 3 + 0], t[i * 3 + 1], t[i * 3 + 2]); }
-RTG_D v3 bilinear(const float* T, int w, int h, float tu, float tv) {
+// texel fetchers: packed RGB (3 floats) or the device layout (RGB + pad, one 16-B load)
+struct Texels3 {
+    const float* t;
+    RTG_D v3 operator()(int i) const { return mk(t[i * 3 + 0], t[i * 3 + 1], t[i * 3 + 2]); }
+};
+struct Texels4 {
+    const float4* t;
+    RTG_D v3 operator()(int i) const { const float4 v = t[i]; return mk(v.x, v.y, v.z); }
+};
+template <class TX>
+RTG_D v3 bilinear(TX texel, int w, int h, float tu, float tv) {
     float au = fabsf(tu), av = fabsf(tv);
     float u = smax(0.0f, au) * (float)w;
     float v = smax(0.0f, av) * (float)h;
@@ -216,13 +225,13 @@ RTG_D v3 bilinear(const float* T, int w, int h, float tu, float tv) {
     x = x < w ? x : x % w;
     y = y < h ? y : y % h;
     const int x1 = (x + 1 == w) ? 0 : x + 1, y1 = (y + 1 == h) ? 0 : y + 1;
-    v3 s0 = texel(T, y * w + x), s1 = texel(T, y * w + x1);
-    v3 s2 = texel(T, y1 * w + x), s3 = texel(T, y1 * w + x1);
+    v3 s0 = texel(y * w + x), s1 = texel(y * w + x1);
+    v3 s2 = texel(y1 * w + x), s3 = texel(y1 * w + x1);
     return add(add(add(muls(s0, w0), muls(s1, w1)), muls(s2, w2)), muls(s3, w3));
 }
 RTG_D v3 tex_sample(const SceneView& s, int tex, float tu, float tv) {
     DevTex ti = s.texinfo[tex];
-    return bilinear(s.texels + (size_t)ti.off * 3, ti.w, ti.h, tu, tv);
+    return bilinear(Texels4{s.texels + ti.off}, ti.w, ti.h, tu, tv);
 }
 
 // ------------------------------------------------------------------ sampling (Sampling.h)

@@ -37,6 +37,9 @@ using namespace rtgd;
 #ifndef RTG_FETCH_TAIL
 #define RTG_FETCH_TAIL 8    // k: fetch 64 rays per atomic once about k rounds of big batches are left
 #endif
+#ifndef RTG_TAIL_BATCH
+#define RTG_TAIL_BATCH 64   // rays per atomic in the tail rounds
+#endif
 #ifndef RTG_FETCH8
 #define RTG_FETCH8 1        // k_trace fetches from 8 slice counters (TraceIO::fetch8): +4 % per GPU at N=8
 #endif

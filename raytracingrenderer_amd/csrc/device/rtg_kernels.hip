@@ -89,7 +89,7 @@ void k_trace(SceneView s, TraceIO io) {
             // slice blockIdx % 8 and moves on to the next slice when its own runs dry.
             while (pool_left == 0) {
                 const bool tail = RTG_FETCH_TAIL && last_b + tail_rays >= s_len;
-                const unsigned g = tail ? 64u : fetch_big;
+                const unsigned g = tail ? (unsigned)RTG_TAIL_BATCH : fetch_big;
                 unsigned b = 0;
                 if (lane == 0) b = atomicAdd(io.fetch8 ? io.fetch8 + 32 * slice : io.fetch, g);
                 b = __shfl(b, 0);
@@ -881,6 +881,8 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                     }
                 } else {
                     const bool spec = M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS;
+                    // albedo->sample(tu, tv): one fetch for BSDF::evaluate (NEE) and BSDF::sample
+                    const v3 alb = tex_sample(s, M.tex, tu, tv);
                     // ---- computeDirect (Renderer.h:423-473)
                     v3 ld = mk(0.0f, 0.0f, 0.0f);
                     if (!spec) {
@@ -921,7 +923,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                             const float maxt = sqrtf(length_sq(sd)) - (2.0f * RTG_EPS);
                             sd = normalize(sd);
                             const v3 so = add(x, muls(sd, RTG_EPS));
-                            const v3 f = divs(tex_sample(s, M.tex, tu, tv), RTG_PI_F);  // BSDF::evaluate
+                            const v3 f = divs(alb, RTG_PI_F);  // BSDF::evaluate
                             ld = divs(muls(mul(f, emitted), g), pmf * pdf);
                             const v3 cvis = mul(thr, ld);
                             p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
@@ -940,7 +942,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                             v3 ind;
                             float pdf;
                             PcgSampler smp{st, inc};
-                            const v3 wi = bsdf_sample(M.kind, M.int_ior, M.ext_ior, tex_sample(s, M.tex, tu, tv), fr, wo,
+                            const v3 wi = bsdf_sample(M.kind, M.int_ior, M.ext_ior, alb, fr, wo,
                                                       smp, ind, pdf);
                             st = smp.s;
                             if (spec) thr = divs(mul(thr, ind), pdf);
@@ -1107,7 +1109,7 @@ __global__ void k_probe_bsdf(const float* in, int n, float* out) {
     if (i >= n) return;
     const float* c = in + (size_t)i * 20;
     const int kind = (int)c[0];
-    const v3 alb = bilinear(c + 3, 1, 1, c[12], c[13]);  // albedo->sample(tu, tv)
+    const v3 alb = bilinear(Texels3{c + 3}, 1, 1, c[12], c[13]);  // albedo->sample(tu, tv)
     const frame fr = frame_from(mk(c[6], c[7], c[8]));
     const v3 wo = mk(c[9], c[10], c[11]);
     ScriptSampler smp{c + 14, 4, 0};
@@ -1503,8 +1505,9 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     for (uint32_t i = 0; i < d->n_textures; ++i) {
         const rtg_texture& t = d->textures[i];
         if (t.width <= 0 || t.height <= 0 || !t.texels) { g_err = "empty texture"; return RTG_ERR_ARG; }
-        texinfo[i] = DevTex{(int)(texels.size() / 3), t.width, t.height, 0};
-        texels.insert(texels.end(), t.texels, t.texels + (size_t)t.width * t.height * 3);
+        texinfo[i] = DevTex{(int)(texels.size() / 4), t.width, t.height, 0};
+        for (size_t j = 0; j < (size_t)t.width * t.height; ++j)  // RGB + pad: one 16-B load per texel
+            texels.insert(texels.end(), {t.texels[3 * j], t.texels[3 * j + 1], t.texels[3 * j + 2], 0.0f});
     }
     if (d->env_texture >= (int)d->n_textures) { g_err = "env texture out of range"; return RTG_ERR_ARG; }
     std::vector<DevLight> lights(d->n_lights);
@@ -1550,7 +1553,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     s.mats = h->d_mats;
     s.lights = h->d_lights;
     s.texinfo = h->d_texinfo;
-    s.texels = h->d_texels;
+    s.texels = (const float4*)h->d_texels;
     s.n_lights = (int)d->n_lights;
     s.env_tex = d->env_texture;
     s.root_word = root_word;
