@@ -40,6 +40,9 @@ using namespace rtgd;
 #ifndef RTG_TAIL_BATCH
 #define RTG_TAIL_BATCH 64   // rays per atomic in the tail rounds
 #endif
+#ifndef RTG_WAVETIME
+#define RTG_WAVETIME 0      // 1: compile k_trace's per-wave clocks (diagnostic; RTG_WAVETIME env then enables)
+#endif
 #ifndef RTG_FETCH8
 #define RTG_FETCH8 1        // k_trace fetches from 8 slice counters (TraceIO::fetch8): +4 % per GPU at N=8
 #endif

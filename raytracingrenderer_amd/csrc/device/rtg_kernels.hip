@@ -67,7 +67,7 @@ void k_trace(SceneView s, TraceIO io) {
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0, pend = RTG_EXIT;
     bool occluded = false, wide = false, anyr = false;  // anyr: this lane's ray is a shadow ray
     const unsigned wslot = gtid >> 6;
-    if (io.wtime && lane == 0) io.wtime[3 * wslot] = __builtin_amdgcn_s_memrealtime();
+    if (RTG_WAVETIME && io.wtime && lane == 0) io.wtime[3 * wslot] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         // ---- retire finished rays
         if (have && cur == RTG_EXIT && pend == RTG_EXIT) {
@@ -92,14 +92,14 @@ void k_trace(SceneView s, TraceIO io) {
                 const unsigned g = tail ? (unsigned)RTG_TAIL_BATCH : fetch_big;
                 unsigned b = 0;
                 if (lane == 0) b = atomicAdd(io.fetch8 ? io.fetch8 + 32 * slice : io.fetch, g);
-                b = __shfl(b, 0);
+                b = __builtin_amdgcn_readfirstlane(b);  // wave-uniform: keeps the fetch state in SGPRs
                 last_b = b;
                 if (b < s_len) {
                     pool_base = s_lo + b;
                     pool_left = min(g, s_len - b);
                 } else if (!io.fetch8 || ++tried == 8) {
                     drained = true;
-                    if (io.wtime && lane == 0) io.wtime[3 * wslot + 1] = __builtin_amdgcn_s_memrealtime();
+                    if (RTG_WAVETIME && io.wtime && lane == 0) io.wtime[3 * wslot + 1] = __builtin_amdgcn_s_memrealtime();
                     break;
                 } else {
                     slice = (slice + 1) & 7;
@@ -439,7 +439,7 @@ void k_trace(SceneView s, TraceIO io) {
         }
 #endif
     }
-    if (io.wtime && lane == 0) io.wtime[3 * wslot + 2] = __builtin_amdgcn_s_memrealtime();
+    if (RTG_WAVETIME && io.wtime && lane == 0) io.wtime[3 * wslot + 2] = __builtin_amdgcn_s_memrealtime();
     if (COUNT) {
         for (int off = 32; off > 0; off >>= 1) {
             c_nodes += __shfl_down(c_nodes, off);

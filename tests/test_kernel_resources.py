@@ -1,0 +1,50 @@
+"""Register budget of the hot kernels (compiled here for gfx950, no GPU needed): a change that
+makes the traversal or shading kernel spill in its loop costs ~15 % (a scratch reload per node
+step is a vector-memory request in a request-bound loop), so the spill counts are pinned."""
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "raytracingrenderer_amd", "csrc", "device", "rtg_kernels.hip")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+@pytest.fixture(scope="module")
+def kernels():
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "k.s")
+        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17",
+                        "--cuda-device-only", "-S", "-o", out, SRC], check=True, capture_output=True)
+        s = open(out).read()
+    md = s[s.index("amdhsa.kernels"):]
+    res = {}
+    for blk in md.split("  - .agpr_count")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+        res[name] = {k: int(re.search(r"\." + k + r":\s+(\d+)", blk).group(1))
+                     for k in ("vgpr_count", "vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size")}
+    return res
+
+
+def _find(kernels, prefix):
+    names = [k for k in kernels if k.startswith(prefix)]
+    assert names, prefix
+    return kernels[names[0]]
+
+
+def test_traversal_fits_six_waves_without_loop_spills(kernels):
+    k = _find(kernels, "_Z7k_traceILb0E")
+    assert k["vgpr_count"] <= 80  # 6 waves per SIMD
+    # two VGPRs of the stack-overflow pointer may live in scratch: they are read only when a lane's
+    # stack is deeper than its 24 LDS entries
+    assert k["vgpr_spill_count"] <= 2, k
+
+
+def test_shading_kernel_does_not_spill(kernels):
+    k = _find(kernels, "_Z7k_shadeILb0E")
+    assert k["vgpr_spill_count"] == 0 and k["private_segment_fixed_size"] == 0, k
