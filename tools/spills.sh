@@ -1,0 +1,18 @@
+#!/bin/bash
+# VGPR / spill counts of k_trace<false> and k_shade<false> for a set of -D flags: spills.sh "-DFOO=1" ...
+for flags in "$@"; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 --cuda-device-only -S $flags \
+    -o /tmp/spills_k.s "$(dirname "$0")/../raytracingrenderer_amd/csrc/device/rtg_kernels.hip" 2>/dev/null
+  python3 - "$flags" <<'PY'
+import re, sys
+s = open('/tmp/spills_k.s').read()
+md = s[s.index('amdhsa.kernels'):]
+out = []
+for blk in md.split('  - .agpr_count')[1:]:
+    name = re.search(r'\.name:\s+(\S+)', blk).group(1)
+    if name.startswith(('_Z7k_traceILb0E', '_Z7k_shadeILb0E')):
+        g = lambda k: re.search(r'\.' + k + r':\s+(\d+)', blk).group(1)
+        out.append('%s v%s/spill%s s-spill%s' % (name[7:14], g('vgpr_count'), g('vgpr_spill_count'), g('sgpr_spill_count')))
+print(repr(sys.argv[1]), ' | '.join(out))
+PY
+done
