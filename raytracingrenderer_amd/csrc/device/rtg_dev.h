@@ -28,6 +28,7 @@
 #define RTG_EPS 1e-4f                    // EPSILON, Geometry.h:60
 #define RTG_PI_F 3.14159274f             // (float)M_PI, as in Colour / M_PI (Materials.h:131)
 #define RTG_EXIT ((int)0x80000000)       // traversal sentinel (never a valid child word)
+#define RTG_LEAF_SPAN 4                  // leaf word = ~(first triangle * RTG_LEAF_SPAN + count - 1)
 
 namespace rtgd {
 

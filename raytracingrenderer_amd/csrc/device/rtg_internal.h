@@ -43,6 +43,9 @@ using namespace rtgd;
 #ifndef RTG_WAVETIME
 #define RTG_WAVETIME 0      // 1: compile k_trace's per-wave clocks (diagnostic; RTG_WAVETIME env then enables)
 #endif
+#ifndef RTG_COLLAPSE_DP
+#define RTG_COLLAPSE_DP 0   // 1: SAH-optimal BVH2 -> 4-wide cut with leaf merging (env RTG_COLLAPSE=dp|greedy)
+#endif
 #ifndef RTG_FETCH8
 #define RTG_FETCH8 1        // k_trace fetches from 8 slice counters (TraceIO::fetch8): +4 % per GPU at N=8
 #endif

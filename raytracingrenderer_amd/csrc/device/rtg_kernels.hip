@@ -151,12 +151,12 @@ void k_trace(SceneView s, TraceIO io) {
             if (!RTG_POSTPONE) c_lstep += (have && cur != RTG_EXIT && cur < 0) ? 1 : 0;
         }
         if (!have || (cur == RTG_EXIT && pend == RTG_EXIT)) continue;
-        // Leaf: the reference's leaf loop (Geometry.h:420-431 / 446-458) over 1-2 triangles.
+        // Leaf: the reference's leaf loop (Geometry.h:420-431 / 446-458) over 1-2 triangles (a wide
+        // leaf slot may join sibling reference leaves: up to RTG_LEAF_SPAN triangles).
         auto leaf = [&](const int word) {
             const int code = ~word;
-            const int start = code >> 1;
-            const int cnt = (code & 1) + 1;
-            bool lchk = false, lok = true;  // exact leaf box, tested on the first candidate only
+            const int start = code / RTG_LEAF_SPAN;  // leaf word ~(start * RTG_LEAF_SPAN + count - 1)
+            const int cnt = (code % RTG_LEAF_SPAN) + 1;
             for (int k = 0; k < cnt; ++k) {
                 const int tri = start + k;
                 if (COUNT) (anyr ? c_stris : c_tris) += 1;
@@ -175,12 +175,10 @@ void k_trace(SceneView s, TraceIO io) {
                                      : (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid)));
 #if RTG_QNODE
                     if (cand && wide) {
-                        if (!lchk) {
-                            const float4 b0 = s.leafbox[2 * start], b1 = s.leafbox[2 * start + 1];
-                            lok = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
-                            lchk = true;
-                        }
-                        cand = lok;
+                        // the exact box of the reference leaf holding this triangle (stored per
+                        // triangle: a wide leaf slot may join sibling reference leaves)
+                        const float4 b0 = s.leafbox[2 * tri], b1 = s.leafbox[2 * tri + 1];
+                        cand = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
                     }
 #endif
                     if (!cand) {
@@ -535,10 +533,9 @@ __global__ __launch_bounds__(RTG_TB) void k_trace_packet(SceneView s, TraceIO io
         // leaf (1-2 triangles) for the lanes of mask m; records through scalar loads
         auto leaf = [&](int word, unsigned long long m) {
             const int code = ~word;
-            const int start = code >> 1;
-            const int cnt = (code & 1) + 1;
+            const int start = code / RTG_LEAF_SPAN;  // leaf word ~(start * RTG_LEAF_SPAN + count - 1)
+            const int cnt = (code % RTG_LEAF_SPAN) + 1;
             const bool mine = (m >> lane) & 1ull;
-            bool lchk = false, lok = true;
             for (int k = 0; k < cnt; ++k) {
                 const int tri = start + k;
                 DevTri48 T;
@@ -549,12 +546,8 @@ __global__ __launch_bounds__(RTG_TB) void k_trace_packet(SceneView s, TraceIO io
                 if (!mine) continue;
                 const bool hit = tri_intersect48(T, o, d, [&](float tt) { return tt <= tbest && tt > RTG_EPS; }, t, u, v);
                 if (hit && t > RTG_EPS && (t < tbest || (t == tbest && tri < bid))) {
-                    if (!lchk) {
-                        const float4 b0 = cload4(s.leafbox + 2 * start, 0), b1 = cload4(s.leafbox + 2 * start, 1);
-                        lok = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
-                        lchk = true;
-                    }
-                    if (lok) {
+                    const float4 b0 = cload4(s.leafbox + 2 * tri, 0), b1 = cload4(s.leafbox + 2 * tri, 1);
+                    if (slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv)) {
                         tbest = t;
                         bid = tri;
                         bu = u;
@@ -1349,7 +1342,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         if (L[0] >= 0) { out = internal_id[node]; return true; }
         int cnt = L[3] - L[2];
         if (cnt < 1 || cnt > 2 || L[2] < 0 || (uint32_t)L[3] > nt) return false;
-        out = ~(L[2] * 2 + (cnt - 1));
+        out = ~(L[2] * RTG_LEAF_SPAN + (cnt - 1));
         return true;
     };
     std::vector<DevNode> nodes(std::max(n_internal, 1));
@@ -1411,6 +1404,99 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             const double x = b[3] - b[0], y = b[4] - b[1], z = b[5] - b[2];
             return x * y + y * z + z * x;
         };
+        // SAH-optimal cut (RTG_COLLAPSE=dp): bottom-up over the BVH2, best[n][k] is the
+        // least expected cost of covering n's subtree with at most k slots, a slot being a
+        // reference leaf, a wide node, or (leaf merge) a subtree of <= RTG_LEAF_SPAN triangles
+        // tested as one leaf; cost = area x (node step | triangles x c_tri). Every slot box still
+        // contains the reference leaf boxes below it, so the exactness argument of k_trace holds.
+        const char* ce = std::getenv("RTG_COLLAPSE");
+        const bool dp = ce ? std::strcmp(ce, "dp") == 0 : RTG_COLLAPSE_DP;
+        const double c_tri = std::getenv("RTG_DP_CTRI") ? std::atof(std::getenv("RTG_DP_CTRI")) : 0.6;
+        const int leaf_max = std::getenv("RTG_DP_LEAF") ? std::atoi(std::getenv("RTG_DP_LEAF")) : RTG_LEAF_SPAN;
+        std::vector<std::array<double, 5>> best;
+        std::vector<std::array<int8_t, 5>> split;  // k >= 2: 0 = as k-1, j = j slots left / k-j right
+        std::vector<int8_t> wsplit, merged;         // wide node: slots given to the left child; merged leaf
+        std::vector<int> lo_tri, n_tri;
+        if (dp) {
+            best.assign(nn, {});
+            split.assign(nn, {});
+            wsplit.assign(nn, 0);
+            merged.assign(nn, 0);
+            lo_tri.assign(nn, 0);
+            n_tri.assign(nn, 0);
+            std::vector<int> order;  // post-order (children first)
+            order.reserve(nn);
+            std::vector<std::pair<int, bool>> st{{0, false}};
+            while (!st.empty()) {
+                auto [i, done] = st.back();
+                st.pop_back();
+                if (done || !internal(i)) { order.push_back(i); continue; }
+                st.push_back({i, true});
+                st.push_back({d->node_links[(size_t)i * 4 + 1], false});
+                st.push_back({d->node_links[(size_t)i * 4], false});
+            }
+            for (int i : order) {
+                const int32_t* L = d->node_links + (size_t)i * 4;
+                const double A = area(i);
+                if (!internal(i)) {
+                    lo_tri[i] = L[2];
+                    n_tri[i] = L[3] - L[2];
+                    for (int k = 1; k <= 4; ++k) best[i][k] = A * c_tri * n_tri[i];
+                    continue;
+                }
+                const int l = L[0], r = L[1];
+                lo_tri[i] = std::min(lo_tri[l], lo_tri[r]);
+                n_tri[i] = n_tri[l] + n_tri[r];
+                const bool contiguous = std::max(lo_tri[l] + n_tri[l], lo_tri[r] + n_tri[r]) - lo_tri[i] == n_tri[i];
+                double cw = 1e300;
+                for (int j = 1; j <= 3; ++j) {
+                    const double c = best[l][j] + best[r][4 - j];
+                    if (c < cw) { cw = c; wsplit[i] = (int8_t)j; }
+                }
+                cw += A;  // one node step
+                double c1 = cw;
+                if (i != 0 && contiguous && n_tri[i] <= leaf_max && A * c_tri * n_tri[i] < cw) {
+                    c1 = A * c_tri * n_tri[i];
+                    merged[i] = 1;
+                }
+                best[i][1] = c1;
+                for (int k = 2; k <= 4; ++k) {
+                    best[i][k] = best[i][k - 1];
+                    for (int j = 1; j < k; ++j) {
+                        const double c = best[l][j] + best[r][k - j];
+                        if (c < best[i][k]) { best[i][k] = c; split[i][k] = (int8_t)j; }
+                    }
+                }
+            }
+        }
+        // the slots of the wide node made from BVH2 node n2: a cut of its subtree below it
+        auto cut = [&](int n2) {
+            std::vector<int> slots;
+            if (dp) {
+                std::vector<std::pair<int, int>> st{{d->node_links[(size_t)n2 * 4 + 1], 4 - wsplit[n2]},
+                                                    {d->node_links[(size_t)n2 * 4], wsplit[n2]}};
+                while (!st.empty()) {
+                    auto [x, k] = st.back();
+                    st.pop_back();
+                    while (k > 1 && split[x][k] == 0) --k;
+                    if (k == 1) { slots.push_back(x); continue; }
+                    st.push_back({d->node_links[(size_t)x * 4 + 1], k - split[x][k]});
+                    st.push_back({d->node_links[(size_t)x * 4], split[x][k]});
+                }
+                return slots;
+            }
+            slots = {d->node_links[(size_t)n2 * 4], d->node_links[(size_t)n2 * 4 + 1]};
+            while ((int)slots.size() < RTG_WIDTH) {
+                int best_k = -1;
+                for (int k = 0; k < (int)slots.size(); ++k)
+                    if (internal(slots[k]) && (best_k < 0 || area(slots[k]) > area(slots[best_k]))) best_k = k;
+                if (best_k < 0) break;
+                const int c = slots[best_k];
+                slots[best_k] = d->node_links[(size_t)c * 4];
+                slots.push_back(d->node_links[(size_t)c * 4 + 1]);
+            }
+            return slots;
+        };
         nodesw.emplace_back();
         nodesq.emplace_back();
         root_wordw = 0;
@@ -1419,20 +1505,13 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             auto [n2, nw, lvl] = work.back();
             work.pop_back();
             h->wide_depth = std::max(h->wide_depth, (uint32_t)lvl);
-            std::vector<int> slots{d->node_links[(size_t)n2 * 4], d->node_links[(size_t)n2 * 4 + 1]};
-            while ((int)slots.size() < RTG_WIDTH) {
-                int best = -1;
-                for (int k = 0; k < (int)slots.size(); ++k)
-                    if (internal(slots[k]) && (best < 0 || area(slots[k]) > area(slots[best]))) best = k;
-                if (best < 0) break;
-                const int c = slots[best];
-                slots[best] = d->node_links[(size_t)c * 4];
-                slots.push_back(d->node_links[(size_t)c * 4 + 1]);
-            }
+            const std::vector<int> slots = cut(n2);
 #if RTG_QNODE
             int32_t wq[4] = {RTG_EXIT, RTG_EXIT, RTG_EXIT, RTG_EXIT};
             for (int k = 0; k < (int)slots.size(); ++k) {
-                if (internal(slots[k])) {
+                if (dp && merged[slots[k]]) {  // one leaf slot for a small subtree
+                    wq[k] = ~(lo_tri[slots[k]] * RTG_LEAF_SPAN + (n_tri[slots[k]] - 1));
+                } else if (internal(slots[k])) {
                     wq[k] = (int)nodesq.size();
                     nodesq.emplace_back();
                     work.push_back({slots[k], wq[k], lvl + 1});

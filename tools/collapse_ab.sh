@@ -1,0 +1,12 @@
+#!/bin/bash
+# BVH2 -> 4-wide collapse variants (RTG_COLLAPSE / RTG_DP_CTRI / RTG_DP_LEAF env): parity suite in dp
+# mode, then C3 bench per variant with the wide walk's slot / triangle tests per ray
+R=$GRAFT_REPO_ROOT; cd $R
+RTG_COLLAPSE=dp timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/dp_pytest.log 2>&1 || { tail -30 gpurun_out/dp_pytest.log; exit 1; }
+tail -1 gpurun_out/dp_pytest.log
+for round in 1 2; do
+for v in "greedy 0.6 4" "dp 0.6 4" "dp 0.6 2" "dp 1.0 4" "dp 0.4 4"; do
+  set -- $v
+  RTG_COLLAPSE=$1 RTG_DP_CTRI=$2 RTG_DP_LEAF=$3 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 3 ${CFG:+--config $CFG} > gpurun_out/col.log 2>&1 || { tail -5 gpurun_out/col.log; exit 1; }
+  echo "$v $(tail -1 gpurun_out/col.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], d['kernel_ms_per_step_rank0'], 'slots', r['walk_box_tests_per_ray'], 'tris', r['walk_tri_tests_per_ray'], 'pops', r['pops_per_ray'])")"
+done; done
