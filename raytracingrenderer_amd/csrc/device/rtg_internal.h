@@ -46,6 +46,9 @@ using namespace rtgd;
 #ifndef RTG_COLLAPSE_DP
 #define RTG_COLLAPSE_DP 0   // 1: SAH-optimal BVH2 -> 4-wide cut with leaf merging (env RTG_COLLAPSE=dp|greedy)
 #endif
+#ifndef RTG_REBUILD
+#define RTG_REBUILD 1       // wide nodes cut from an own 3-axis SAH tree over the reference leaves (env RTG_REBUILD=0: from the reference BVH2)
+#endif
 #ifndef RTG_FETCH8
 #define RTG_FETCH8 1        // k_trace fetches from 8 slice counters (TraceIO::fetch8): +4 % per GPU at N=8
 #endif
@@ -198,6 +201,7 @@ struct rtg_handle {
     float4* d_leafbox = nullptr;
     int usew = 0, wide = 1;
     int integrator = RTG_INTEGRATOR_PATH;
+    bool rebuilt = false;     // wide tree cut from rebuild_over_leaves (RTG_REBUILD)
     uint32_t wide_depth = 0;  // wide levels on the longest root-to-leaf path
     DevTri* d_tris = nullptr;
     DevTri48* d_tris48 = nullptr;

@@ -1263,6 +1263,126 @@ static void host_cross(const float* a, const float* b, float* o) {
     o[2] = (a[0] * b[1]) - (a[1] * b[0]);
 }
 
+// Own binary SAH tree over the reference's leaves (RTG_REBUILD=1), in the descriptor's node format
+// (links {left, right, start, end}, bounds {min xyz, max xyz}; node 0 is the root). Primitives are
+// the reference leaves with their exact boxes, kept whole, so the wide walk built from this tree
+// still reaches every leaf whose box passes (internal boxes are float min/max unions: containment
+// is exact) and k_trace's leaf-box test keeps reachability the reference's. The reference splits
+// along the longest axis only (Geometry.h:343-386); this build tries all three: full SAH sweep
+// below 2048 leaves, 64 centroid bins per axis above.
+static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& lk, std::vector<float>& bd) {
+    std::vector<int> leaf;
+    for (uint32_t i = 0; i < d->n_nodes; ++i)
+        if (d->node_links[(size_t)i * 4] < 0) leaf.push_back((int)i);
+    const size_t n = leaf.size();
+    if (n < 2) return false;
+    auto box = [&](int p) { return d->node_bounds + (size_t)leaf[p] * 6; };
+    std::vector<float> cen(n * 3);
+    for (size_t p = 0; p < n; ++p)
+        for (int a = 0; a < 3; ++a) cen[p * 3 + a] = 0.5f * (box((int)p)[a] + box((int)p)[a + 3]);
+    struct Bx {
+        float b[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        void add(const float* o) {
+            for (int a = 0; a < 3; ++a) { b[a] = std::min(b[a], o[a]); b[a + 3] = std::max(b[a + 3], o[a + 3]); }
+        }
+        double area() const {
+            if (b[0] > b[3]) return 0.0;
+            const double x = (double)b[3] - b[0], y = (double)b[4] - b[1], z = (double)b[5] - b[2];
+            return x * y + y * z + z * x;
+        }
+    };
+    std::vector<int> idx(n);
+    for (size_t p = 0; p < n; ++p) idx[p] = (int)p;
+    lk.assign((2 * n - 1) * 4, -1);
+    bd.assign((2 * n - 1) * 6, 0.0f);
+    int next = 1;
+    std::vector<std::array<int, 4>> st{{0, 0, (int)n, 0}};  // node id, range [lo, hi) of idx, depth
+    std::vector<Bx> suf;
+    while (!st.empty()) {
+        auto [node, lo, hi, dep] = st.back();
+        st.pop_back();
+        if (dep > 96) return false;  // degenerate SAH chain: keep the reference tree (bounded stacks)
+        const int m = hi - lo;
+        Bx all;
+        for (int p = lo; p < hi; ++p) all.add(box(idx[p]));
+        std::memcpy(&bd[(size_t)node * 6], all.b, sizeof(all.b));
+        if (m == 1) {
+            const int32_t* L = d->node_links + (size_t)leaf[idx[lo]] * 4;
+            std::memcpy(&lk[(size_t)node * 4], L, 4 * sizeof(int32_t));
+            continue;
+        }
+        double best = INFINITY;
+        int bax = -1, bsplit = lo + m / 2;  // fallback: median of the current order
+        int bbin = 0;
+        if (m <= 2048) {
+            for (int a = 0; a < 3; ++a) {
+                std::sort(idx.begin() + lo, idx.begin() + hi, [&](int x, int y) {
+                    return cen[x * 3 + a] < cen[y * 3 + a] || (cen[x * 3 + a] == cen[y * 3 + a] && x < y);
+                });
+                suf.assign(m + 1, Bx());
+                for (int p = m - 1; p >= 0; --p) { suf[p] = suf[p + 1]; suf[p].add(box(idx[lo + p])); }
+                Bx left;
+                for (int p = 1; p < m; ++p) {
+                    left.add(box(idx[lo + p - 1]));
+                    const double c = left.area() * p + suf[p].area() * (m - p);
+                    if (c < best) { best = c; bax = a; bsplit = lo + p; }
+                }
+            }
+            if (bax >= 0) {
+                std::sort(idx.begin() + lo, idx.begin() + hi, [&](int x, int y) {
+                    return cen[x * 3 + bax] < cen[y * 3 + bax] || (cen[x * 3 + bax] == cen[y * 3 + bax] && x < y);
+                });
+            }
+        } else {
+            constexpr int NB = 64;
+            Bx cb;
+            for (int p = lo; p < hi; ++p) {
+                const float* c = &cen[(size_t)idx[p] * 3];
+                const float cc[6] = {c[0], c[1], c[2], c[0], c[1], c[2]};
+                cb.add(cc);
+            }
+            for (int a = 0; a < 3; ++a) {
+                const float ext = cb.b[a + 3] - cb.b[a];
+                if (!(ext > 0.0f)) continue;
+                Bx bins[NB];
+                int cnt[NB] = {};
+                for (int p = lo; p < hi; ++p) {
+                    const int b = std::min(NB - 1, (int)((cen[(size_t)idx[p] * 3 + a] - cb.b[a]) / ext * NB));
+                    bins[b].add(box(idx[p]));
+                    ++cnt[b];
+                }
+                Bx right[NB + 1];
+                int rc[NB + 1] = {};
+                for (int b = NB - 1; b >= 0; --b) { right[b] = right[b + 1]; right[b].add(bins[b].b); rc[b] = rc[b + 1] + cnt[b]; }
+                Bx left;
+                int lc = 0;
+                for (int b = 1; b < NB; ++b) {
+                    left.add(bins[b - 1].b);
+                    lc += cnt[b - 1];
+                    if (lc == 0 || rc[b] == 0) continue;
+                    const double c = left.area() * lc + right[b].area() * rc[b];
+                    if (c < best) { best = c; bax = a; bbin = b; }
+                }
+            }
+            if (bax >= 0) {
+                const float ext = cb.b[bax + 3] - cb.b[bax];
+                auto mid = std::partition(idx.begin() + lo, idx.begin() + hi, [&](int x) {
+                    return std::min(NB - 1, (int)((cen[(size_t)x * 3 + bax] - cb.b[bax]) / ext * NB)) < bbin;
+                });
+                bsplit = (int)(mid - idx.begin());
+                if (bsplit == lo || bsplit == hi) bsplit = lo + m / 2;
+            }
+        }
+        const int l = next++, r = next++;
+        lk[(size_t)node * 4] = l;
+        lk[(size_t)node * 4 + 1] = r;
+        lk[(size_t)node * 4 + 2] = lk[(size_t)node * 4 + 3] = 0;
+        st.push_back({r, bsplit, hi, dep + 1});
+        st.push_back({l, lo, bsplit, dep + 1});
+    }
+    return next == (int)(2 * n - 1);
+}
+
 extern "C" {
 
 int32_t rtg_abi_version(void) { return RTG_ABI_VERSION; }
@@ -1398,9 +1518,26 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         }
     }
     if (nt > 0 && finite && d->node_links[0] >= 0) {
-        auto internal = [&](int i) { return d->node_links[(size_t)i * 4] >= 0; };
+        // the tree the wide nodes are cut from: the reference BVH2, or (RTG_REBUILD=1) an own SAH
+        // tree over the reference's leaves (rebuild_over_leaves)
+        std::vector<int32_t> rlk;
+        std::vector<float> rbd;
+        const char* rb_env = std::getenv("RTG_REBUILD");
+        const bool rebuilt = (rb_env ? std::atoi(rb_env) != 0 : RTG_REBUILD) && rebuild_over_leaves(d, rlk, rbd);
+        const int32_t* LK = rebuilt ? rlk.data() : d->node_links;
+        const float* BD = rebuilt ? rbd.data() : d->node_bounds;
+        const uint32_t nn = rebuilt ? (uint32_t)(rlk.size() / 4) : d->n_nodes;
+        auto wordw = [&](int node, int& out) -> bool {  // leaf word (leaves are the reference's)
+            const int32_t* L = LK + (size_t)node * 4;
+            const int cnt = L[3] - L[2];
+            if (L[0] >= 0 || cnt < 1 || cnt > 2 || L[2] < 0 || (uint32_t)L[3] > nt) return false;
+            out = ~(L[2] * RTG_LEAF_SPAN + (cnt - 1));
+            return true;
+        };
+        h->rebuilt = rebuilt;
+        auto internal = [&](int i) { return LK[(size_t)i * 4] >= 0; };
         auto area = [&](int i) {
-            const float* b = d->node_bounds + (size_t)i * 6;
+            const float* b = BD + (size_t)i * 6;
             const double x = b[3] - b[0], y = b[4] - b[1], z = b[5] - b[2];
             return x * y + y * z + z * x;
         };
@@ -1432,11 +1569,11 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
                 st.pop_back();
                 if (done || !internal(i)) { order.push_back(i); continue; }
                 st.push_back({i, true});
-                st.push_back({d->node_links[(size_t)i * 4 + 1], false});
-                st.push_back({d->node_links[(size_t)i * 4], false});
+                st.push_back({LK[(size_t)i * 4 + 1], false});
+                st.push_back({LK[(size_t)i * 4], false});
             }
             for (int i : order) {
-                const int32_t* L = d->node_links + (size_t)i * 4;
+                const int32_t* L = LK + (size_t)i * 4;
                 const double A = area(i);
                 if (!internal(i)) {
                     lo_tri[i] = L[2];
@@ -1473,27 +1610,27 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         auto cut = [&](int n2) {
             std::vector<int> slots;
             if (dp) {
-                std::vector<std::pair<int, int>> st{{d->node_links[(size_t)n2 * 4 + 1], 4 - wsplit[n2]},
-                                                    {d->node_links[(size_t)n2 * 4], wsplit[n2]}};
+                std::vector<std::pair<int, int>> st{{LK[(size_t)n2 * 4 + 1], 4 - wsplit[n2]},
+                                                    {LK[(size_t)n2 * 4], wsplit[n2]}};
                 while (!st.empty()) {
                     auto [x, k] = st.back();
                     st.pop_back();
                     while (k > 1 && split[x][k] == 0) --k;
                     if (k == 1) { slots.push_back(x); continue; }
-                    st.push_back({d->node_links[(size_t)x * 4 + 1], k - split[x][k]});
-                    st.push_back({d->node_links[(size_t)x * 4], split[x][k]});
+                    st.push_back({LK[(size_t)x * 4 + 1], k - split[x][k]});
+                    st.push_back({LK[(size_t)x * 4], split[x][k]});
                 }
                 return slots;
             }
-            slots = {d->node_links[(size_t)n2 * 4], d->node_links[(size_t)n2 * 4 + 1]};
+            slots = {LK[(size_t)n2 * 4], LK[(size_t)n2 * 4 + 1]};
             while ((int)slots.size() < RTG_WIDTH) {
                 int best_k = -1;
                 for (int k = 0; k < (int)slots.size(); ++k)
                     if (internal(slots[k]) && (best_k < 0 || area(slots[k]) > area(slots[best_k]))) best_k = k;
                 if (best_k < 0) break;
                 const int c = slots[best_k];
-                slots[best_k] = d->node_links[(size_t)c * 4];
-                slots.push_back(d->node_links[(size_t)c * 4 + 1]);
+                slots[best_k] = LK[(size_t)c * 4];
+                slots.push_back(LK[(size_t)c * 4 + 1]);
             }
             return slots;
         };
@@ -1515,12 +1652,12 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
                     wq[k] = (int)nodesq.size();
                     nodesq.emplace_back();
                     work.push_back({slots[k], wq[k], lvl + 1});
-                } else if (!word(slots[k], wq[k])) {
+                } else if (!wordw(slots[k], wq[k])) {
                     g_err = "bad BVH leaf";
                     return RTG_ERR_ARG;
                 }
             }
-            if (!encode_qnode(d->node_bounds, slots, wq, nodesq[nw])) { qok = false; break; }
+            if (!encode_qnode(BD, slots, wq, nodesq[nw])) { qok = false; break; }
             continue;
 #endif
             float f[RTG_WNODE_F4 * 4];
@@ -1528,13 +1665,13 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             for (int k = 0; k < RTG_WNODE_F4 * 4; ++k) f[k] = 0.0f;
             for (int k = 0; k < RTG_WIDTH; ++k) wdw[k] = RTG_EXIT;
             for (int k = 0; k < (int)slots.size(); ++k) {
-                const float* bb = d->node_bounds + (size_t)slots[k] * 6;
+                const float* bb = BD + (size_t)slots[k] * 6;
                 for (int q = 0; q < 6; ++q) f[q * RTG_WIDTH + k] = bb[q];
                 if (internal(slots[k])) {
                     wdw[k] = (int)nodesw.size();
                     nodesw.emplace_back();
                     work.push_back({slots[k], wdw[k], lvl + 1});
-                } else if (!word(slots[k], wdw[k])) {
+                } else if (!wordw(slots[k], wdw[k])) {
                     g_err = "bad BVH leaf";
                     return RTG_ERR_ARG;
                 }

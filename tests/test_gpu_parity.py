@@ -80,6 +80,28 @@ def test_wide_walk_is_exact(cornell256, synth20k):
         assert np.array_equal(a.trace_visible(r), b.trace_visible(r))
 
 
+@pytest.mark.parametrize("rebuild", ["0", "1"])
+def test_wide_walk_tree_source(rebuild, synth20k, cornell256, monkeypatch):
+    """Wide nodes cut from the reference BVH2 (RTG_REBUILD=0) or from the own 3-axis SAH tree over
+    the reference leaves (RTG_REBUILD=1, the default): both return the BVH2 walk's bits."""
+    monkeypatch.setenv("RTG_REBUILD", rebuild)
+    rng = np.random.default_rng(31)
+    for s in (synth20k, cornell256):
+        assert_bitexact(gpu_film(s, 2, wide=True), gpu_film(s, 2, wide=False), "bvh4 vs bvh2 film")
+        lo, hi = s.node_bounds[0, 0:3], s.node_bounds[0, 3:6]
+        n = 100000
+        r = np.zeros((n, 8), np.float32)
+        r[:, :3] = rng.uniform(lo - 0.1 * (hi - lo), hi + 0.1 * (hi - lo), (n, 3))
+        d = rng.normal(size=(n, 3)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        r[:, 4:7] = d
+        r[:, 3] = np.float32(np.abs(hi - lo).max() * 2)
+        a = RayTracer(s, wide=True)
+        b = RayTracer(s, wide=False)
+        assert_bitexact(a.trace_closest(r), b.trace_closest(r), "bvh4 vs bvh2 closest")
+        assert np.array_equal(a.trace_visible(r), b.trace_visible(r))
+
+
 def test_wide_walk_adversarial_rays(synth20k, cornell256):
     """Rays that start on reference box faces/corners and run (nearly) along box planes: the
     compressed walk's conservative slot test must never lose a reachable leaf."""
