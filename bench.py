@@ -274,7 +274,7 @@ def main():
                          "limiter": "vector-memory address/L1 request rate (TA busy ~87 %); the scene is "
                                     "served from L2/Infinity Cache, so algorithmic bytes can exceed the HBM "
                                     "peak (DESIGN.md §4)",
-                         "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from the reference BVH2)",
+                         "walk": "bvh2" if a.bvh2 else ("bvh4 (collapsed from the reference BVH2)" if os.environ.get("RTG_REBUILD") == "0" else "bvh4 (collapsed from an own 3-axis SAH tree over the reference leaves)"),
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
                          "pops_per_ray": round(cw["pops"] / max(cw["extension_rays"], 1), 2),
