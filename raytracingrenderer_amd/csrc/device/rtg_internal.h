@@ -46,6 +46,9 @@ using namespace rtgd;
 #ifndef RTG_COLLAPSE_DP
 #define RTG_COLLAPSE_DP 0   // 1: SAH-optimal BVH2 -> 4-wide cut with leaf merging (env RTG_COLLAPSE=dp|greedy)
 #endif
+#ifndef RTG_SHADE_PF
+#define RTG_SHADE_PF 0      // 1: k_shade loads the next iteration's path id one iteration ahead
+#endif
 #ifndef RTG_REBUILD
 #define RTG_REBUILD 1       // wide nodes cut from an own 3-axis SAH tree over the reference leaves (env RTG_REBUILD=0: from the reference BVH2)
 #endif

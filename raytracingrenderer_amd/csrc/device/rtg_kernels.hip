@@ -687,9 +687,20 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
     unsigned* qout = p.q[(b + 1) & 1];
     float4* contrib = p.contrib + (size_t)b * a.P;
     // block-uniform loop: all waves of a block take part in every compaction round
+#if RTG_SHADE_PF
+    // the next iteration's path id is loaded one iteration ahead (it heads the dependent chain
+    // id -> payload -> shading record -> texture)
+    unsigned pf_i = blockIdx.x * RTG_TB + threadIdx.x;
+    int pid_next = pf_i < n ? (int)qin[pf_i] : 0;
+#endif
     for (unsigned base = blockIdx.x * RTG_TB; base < n; base += gridDim.x * RTG_TB) {
         const unsigned i = base + threadIdx.x;
         int pid = 0;
+#if RTG_SHADE_PF
+        pid = pid_next;
+        pf_i = i + gridDim.x * RTG_TB;
+        pid_next = pf_i < n ? (int)qin[pf_i] : 0;
+#endif
         bool want_ext = false, want_sh = false;
         bool valid = i < n;
 #if RTG_SHADE_SORT
@@ -722,7 +733,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
         }
 #endif
         if (valid) {
-#if !RTG_SHADE_SORT
+#if !RTG_SHADE_SORT && !RTG_SHADE_PF
             pid = (int)qin[i];
 #endif
             const float4 ro = p.ray_o[pid], rd = p.ray_d[pid];

@@ -321,6 +321,31 @@ def test_deep_bvh_stack_overflow(tmp_path, base):
         assert np.array_equal(rt.trace_visible(r), o.trace_visible(r))
 
 
+@pytest.mark.parametrize("n_copies", [40, 1500])
+def test_coincident_triangles_tree_rebuild(tmp_path, n_copies):
+    """Many copies of one triangle plus random ones: the own SAH tree over the reference leaves
+    (RTG_REBUILD) sees zero centroid extent and equal SAH costs; with 1500 copies the equal-cost
+    splits can chain past the rebuild's depth guard, which falls back to the reference cut.
+    Closest hits (ties broken by the lowest index) and visibility equal the oracle either way."""
+    from raytracingrenderer_amd.renderer import write_mesh_scene
+    rng = np.random.default_rng(5)
+    tri = np.array([(-0.5, -0.5, 0.0), (0.5, -0.5, 0.0), (0.0, 0.5, 0.0)], np.float32)
+    rnd = rng.uniform(-1, 1, (500, 1, 3)) + rng.uniform(-0.1, 0.1, (500, 3, 3))
+    P = np.concatenate([np.repeat(tri[None], n_copies, 0), rnd.astype(np.float32)], 0)
+    s = loadScene(write_mesh_scene(str(tmp_path), P, 32, 32))
+    n = 20000
+    r = np.zeros((n, 8), np.float32)
+    r[:, :3] = rng.uniform(-1.2, 1.2, (n, 3))
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[: n // 2] = -r[: n // 2, :3] + rng.uniform(-0.3, 0.3, (n // 2, 3)).astype(np.float32)  # aim at the copies
+    r[:, 4:7] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    r[:, 3] = np.float32(10.0)
+    o = Oracle(s, 4, "rtm")
+    rt = RayTracer(s)
+    assert_bitexact(rt.trace_closest(r), o.trace_closest(r), "coincident closest")
+    assert np.array_equal(rt.trace_visible(r), o.trace_visible(r))
+
+
 def test_adaptive_render_matches_oracle():
     """RayTracer::adaptiveRender (Renderer.h:583-749): per-tile variance, weights and sample counts,
     and the film of mean-of-samples splats, bit-exact against the oracle (partial tiles included)."""
