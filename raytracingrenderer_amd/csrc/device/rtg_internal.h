@@ -46,6 +46,9 @@ using namespace rtgd;
 #ifndef RTG_COLLAPSE_DP
 #define RTG_COLLAPSE_DP 0   // 1: SAH-optimal BVH2 -> 4-wide cut with leaf merging (env RTG_COLLAPSE=dp|greedy)
 #endif
+#ifndef RTG_SHC_SPEC
+#define RTG_SHC_SPEC 1      // k_shade stores the NEE value in contrib up front; k_trace clears it on occlusion
+#endif
 #ifndef RTG_SHADE_PF
 #define RTG_SHADE_PF 0      // 1: k_shade loads the next iteration's path id one iteration ahead
 #endif

@@ -73,7 +73,8 @@ void k_trace(SceneView s, TraceIO io) {
         if (have && cur == RTG_EXIT && pend == RTG_EXIT) {
             if (anyr) {
                 if (io.visible) io.visible[pid] = occluded ? 0 : 1;
-                else if (!occluded) io.contrib[pid] = io.sray_c[pid];
+                else if (bid == -2 ? occluded : !occluded)
+                    io.contrib[pid] = bid == -2 ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : io.sray_c[pid];
             } else {
                 io.hits[pid] = make_float4(tbest, __int_as_float(bid), bu, bv);
             }
@@ -118,6 +119,9 @@ void k_trace(SceneView s, TraceIO io) {
                     pid = (int)(anyr ? io.squeue[ri - nc] : io.queue[ri]);
                     const float4 ro = anyr ? io.sray_o[pid] : io.ray_o[pid];
                     const float4 rd = anyr ? io.sray_d[pid] : io.ray_d[pid];
+                    // sh_d.w != 0: the shadow value is in sray_c and is copied on visibility;
+                    // 0: k_shade already stored it in contrib, which is cleared on occlusion
+                    // (kept in bid, which a shadow ray does not use: -2 = value already in contrib)
                     o = mk(ro.x, ro.y, ro.z);
                     d = mk(rd.x, rd.y, rd.z);
                     tbest = anyr ? ro.w : RTG_FLT_MAX;
@@ -125,7 +129,7 @@ void k_trace(SceneView s, TraceIO io) {
                     omag = s.cull_scale + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
                     dmag = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
                     delta = RTG_CULL_REL * (omag + (tbest < RTG_FLT_MAX ? tbest * dmag : 0.0f));
-                    bid = -1;
+                    bid = (RTG_SHC_SPEC && anyr && !io.visible && rd.w == 0.0f) ? -2 : -1;
                     bu = bv = 0.0f;
                     occluded = false;
                     sp = 0;
@@ -843,7 +847,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                                 sd = normalize(sd);
                                 const v3 so = add(x, muls(sd, RTG_EPS));
                                 p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
-                                p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 0.0f);
+                                p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 1.0f);  // copy sh_c if visible
                                 p.sh_c[pid] = make_float4(r.x, r.y, r.z, 0.0f);
                                 want_sh = true;
                             }
@@ -861,7 +865,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                                 sd = normalize(sd);
                                 const v3 so = add(x, muls(sd, RTG_EPS));
                                 p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
-                                p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 0.0f);
+                                p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 1.0f);  // copy sh_c if visible
                                 p.sh_c[pid] = make_float4(r.x, r.y, r.z, 1.0f);  // .w: env sample visible
                                 want_sh = true;
                                 env_flag = 1.0f;
@@ -889,6 +893,8 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                     const v3 alb = tex_sample(s, M.tex, tu, tv);
                     // ---- computeDirect (Renderer.h:423-473)
                     v3 ld = mk(0.0f, 0.0f, 0.0f);
+                    bool ld_pre = false;  // contrib takes the visible NEE value now (RTG_SHC_SPEC)
+                    v3 cpre = ld;
                     if (!spec) {
                         const int nl = s.n_lights;
                         const float pmf = 1.f / (float)nl;
@@ -931,13 +937,20 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                             ld = divs(muls(mul(f, emitted), g), pmf * pdf);
                             const v3 cvis = mul(thr, ld);
                             p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
-                            p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 0.0f);
-                            p.sh_c[pid] = make_float4(cvis.x, cvis.y, cvis.z, 0.0f);
+                            // Visible is the common case: contrib takes thr * Ld now and k_trace
+                            // writes thr * 0 = +0 on occlusion. When thr * 0 is not +0 (a non-finite
+                            // throughput) the value goes through sh_c and is copied on visibility.
+                            const v3 z = mul(thr, mk(0.0f, 0.0f, 0.0f));
+                            const bool plain = RTG_SHC_SPEC && (__float_as_uint(z.x) | __float_as_uint(z.y) | __float_as_uint(z.z)) == 0u;
+                            p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, plain ? 0.0f : 1.0f);
+                            if (!plain) p.sh_c[pid] = make_float4(cvis.x, cvis.y, cvis.z, 0.0f);
+                            ld_pre = plain;
+                            cpre = cvis;
                             want_sh = true;
                         }
                     }
                     // direct = thr * Ld, with Ld = 0 until the shadow ray says visible
-                    c = mul(thr, mk(0.0f, 0.0f, 0.0f));
+                    c = ld_pre ? cpre : mul(thr, mk(0.0f, 0.0f, 0.0f));
                     if ((!ALT || a.mode == RTG_INTEGRATOR_PATH) && b <= a.max_depth) {
                         const float rrp = wmin(lum(thr), 0.9f);
                         if (pcg_next(st, inc) < rrp) {
