@@ -1315,6 +1315,19 @@ static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& l
             return x * y + y * z + z * x;
         }
     };
+    // SAH weight of a leaf: its triangle count (1-2), or 1 per leaf (RTG_RB_WEIGHT=0); full sweep
+    // below RTG_RB_SWEEP leaves, RTG_RB_BINS centroid bins per axis above
+    const char* ew = std::getenv("RTG_RB_WEIGHT");
+    const char* es = std::getenv("RTG_RB_SWEEP");
+    const char* eb = std::getenv("RTG_RB_BINS");
+    const bool by_tris = ew ? std::atoi(ew) != 0 : true;
+    const int sweep_max = es ? std::max(2, std::atoi(es)) : 2048;
+    const int nbins = eb ? std::min(256, std::max(4, std::atoi(eb))) : 64;
+    std::vector<double> wt(n), pre;
+    for (size_t p = 0; p < n; ++p) {
+        const int32_t* L = d->node_links + (size_t)leaf[p] * 4;
+        wt[p] = by_tris ? (double)(L[3] - L[2]) : 1.0;
+    }
     std::vector<int> idx(n);
     for (size_t p = 0; p < n; ++p) idx[p] = (int)p;
     lk.assign((2 * n - 1) * 4, -1);
@@ -1338,17 +1351,19 @@ static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& l
         double best = INFINITY;
         int bax = -1, bsplit = lo + m / 2;  // fallback: median of the current order
         int bbin = 0;
-        if (m <= 2048) {
+        if (m <= sweep_max) {
             for (int a = 0; a < 3; ++a) {
                 std::sort(idx.begin() + lo, idx.begin() + hi, [&](int x, int y) {
                     return cen[x * 3 + a] < cen[y * 3 + a] || (cen[x * 3 + a] == cen[y * 3 + a] && x < y);
                 });
                 suf.assign(m + 1, Bx());
                 for (int p = m - 1; p >= 0; --p) { suf[p] = suf[p + 1]; suf[p].add(box(idx[lo + p])); }
+                pre.assign(m + 1, 0.0);
+                for (int p = 0; p < m; ++p) pre[p + 1] = pre[p] + wt[idx[lo + p]];
                 Bx left;
                 for (int p = 1; p < m; ++p) {
                     left.add(box(idx[lo + p - 1]));
-                    const double c = left.area() * p + suf[p].area() * (m - p);
+                    const double c = left.area() * pre[p] + suf[p].area() * (pre[m] - pre[p]);
                     if (c < best) { best = c; bax = a; bsplit = lo + p; }
                 }
             }
@@ -1358,7 +1373,7 @@ static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& l
                 });
             }
         } else {
-            constexpr int NB = 64;
+            const int NB = nbins;
             Bx cb;
             for (int p = lo; p < hi; ++p) {
                 const float* c = &cen[(size_t)idx[p] * 3];
@@ -1368,18 +1383,16 @@ static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& l
             for (int a = 0; a < 3; ++a) {
                 const float ext = cb.b[a + 3] - cb.b[a];
                 if (!(ext > 0.0f)) continue;
-                Bx bins[NB];
-                int cnt[NB] = {};
+                std::vector<Bx> bins(NB), right(NB + 1);
+                std::vector<double> cnt(NB, 0.0), rc(NB + 1, 0.0);
                 for (int p = lo; p < hi; ++p) {
                     const int b = std::min(NB - 1, (int)((cen[(size_t)idx[p] * 3 + a] - cb.b[a]) / ext * NB));
                     bins[b].add(box(idx[p]));
-                    ++cnt[b];
+                    cnt[b] += wt[idx[p]];
                 }
-                Bx right[NB + 1];
-                int rc[NB + 1] = {};
                 for (int b = NB - 1; b >= 0; --b) { right[b] = right[b + 1]; right[b].add(bins[b].b); rc[b] = rc[b + 1] + cnt[b]; }
                 Bx left;
-                int lc = 0;
+                double lc = 0;
                 for (int b = 1; b < NB; ++b) {
                     left.add(bins[b - 1].b);
                     lc += cnt[b - 1];
