@@ -46,6 +46,9 @@ using namespace rtgd;
 #ifndef RTG_COLLAPSE_DP
 #define RTG_COLLAPSE_DP 0   // 1: SAH-optimal BVH2 -> 4-wide cut with leaf merging (env RTG_COLLAPSE=dp|greedy)
 #endif
+#ifndef RTG_GEN_LEAN
+#define RTG_GEN_LEAN 1      // bounce-0 path state implied instead of written by k_generate (ChunkArgs::lean)
+#endif
 #ifndef RTG_SHC_SPEC
 #define RTG_SHC_SPEC 1      // k_shade stores the NEE value in contrib up front; k_trace clears it on occlusion
 #endif
@@ -120,6 +123,8 @@ struct TraceIO {
     int cull;
     int wide;                  // traverse the 4-wide tree when the ray allows it
     unsigned long long* wtime; // diagnostics (RTG_WAVETIME): per wave start / drained / exit clock
+    float4 cam_o;              // closest: the origin of every ray when ray_o is null (camera rays);
+                               // a null queue is the identity (path id = ray index)
 };
 
 struct ChunkArgs {
@@ -130,6 +135,8 @@ struct ChunkArgs {
     int mode;                  // RTG_INTEGRATOR_* (first-hit estimators never continue a path)
     int pm;                    // path id order: 1 pixel-major (pid = lp * ns + sl), 0 sample-major
     DevCamera cam;
+    int lean = 0;              // 1: bounce-0 state implied (identity queue, camera origin, thr 1,
+                               // PCG seed, canHitLight); k_generate writes ray_d only
 };
 
 struct PathBufs {

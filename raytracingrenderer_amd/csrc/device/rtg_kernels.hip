@@ -116,8 +116,8 @@ void k_trace(SceneView s, TraceIO io) {
                     ri = pool_base + pos;
                     have = true;
                     anyr = ri >= nc;
-                    pid = (int)(anyr ? io.squeue[ri - nc] : io.queue[ri]);
-                    const float4 ro = anyr ? io.sray_o[pid] : io.ray_o[pid];
+                    pid = (int)(anyr ? io.squeue[ri - nc] : (io.queue ? io.queue[ri] : ri));
+                    const float4 ro = anyr ? io.sray_o[pid] : (io.ray_o ? io.ray_o[pid] : io.cam_o);
                     const float4 rd = anyr ? io.sray_d[pid] : io.ray_d[pid];
                     // sh_d.w != 0: the shadow value is in sray_c and is copied on visibility;
                     // 0: k_shade already stored it in contrib, which is cleared on occlusion
@@ -662,8 +662,9 @@ __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
              (dir.x * c[4] + dir.y * c[5]) + dir.z * c[6],
              (dir.x * c[8] + dir.y * c[9]) + dir.z * c[10]);
     dir = normalize(dir);
-    p.ray_o[pid] = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f);
     p.ray_d[pid] = make_float4(dir.x, dir.y, dir.z, 0.0f);
+    if (a.lean) return;  // the rest is implied at bounce 0 (k_trace: io.cam_o / identity queue; k_shade)
+    p.ray_o[pid] = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f);
     p.q[0][pid] = pid;
     p.thr[pid] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
     p.rng[pid] = pcg_seed(a.seed, pcg_inc(pixel, a.s0 + sl));
@@ -690,6 +691,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
     const unsigned* qin = p.q[b & 1];
     unsigned* qout = p.q[(b + 1) & 1];
     float4* contrib = p.contrib + (size_t)b * a.P;
+    const bool lean0 = a.lean && b == 0;  // bounce 0: identity queue, state as k_generate would write it
     // block-uniform loop: all waves of a block take part in every compaction round
 #if RTG_SHADE_PF
     // the next iteration's path id is loaded one iteration ahead (it heads the dependent chain
@@ -712,7 +714,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             // stable block-level partition of the 256 path ids: misses first, then hits, so that
             // waves run the miss branch (background lookup) and the surface branch without lane
             // divergence between them (at most one wave holds both)
-            const int p0 = valid ? (int)qin[i] : 0;
+            const int p0 = valid ? (lean0 ? (int)i : (int)qin[i]) : 0;
             const bool miss = valid && !(p.hits[p0].x < RTG_FLT_MAX);
             const unsigned long long mm = __ballot(miss), mh = __ballot(valid && !miss);
             if (lane == 0) {
@@ -738,18 +740,19 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
 #endif
         if (valid) {
 #if !RTG_SHADE_SORT && !RTG_SHADE_PF
-            pid = (int)qin[i];
+            pid = lean0 ? (int)i : (int)qin[i];
 #endif
-            const float4 ro = p.ray_o[pid], rd = p.ray_d[pid];
+            const float4 ro = lean0 ? make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f) : p.ray_o[pid];
+            const float4 rd = p.ray_d[pid];
             const float4 h = p.hits[pid];
             const v3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
-            const float4 thr4 = p.thr[pid];
+            const float4 thr4 = lean0 ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : p.thr[pid];
             v3 thr = mk(thr4.x, thr4.y, thr4.z);
-            const int can_hit = (p.meta[pid] >> 8) & 1;
+            const int can_hit = lean0 ? 1 : (p.meta[pid] >> 8) & 1;
             const unsigned lp = a.pm ? (unsigned)pid / a.ns : (unsigned)pid % a.npix;
             const unsigned sl = a.pm ? (unsigned)pid % a.ns : (unsigned)pid / a.npix;
             const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);
-            uint64_t st = p.rng[pid];
+            uint64_t st = lean0 ? pcg_seed(a.seed, inc) : p.rng[pid];
             v3 c;
             int nterms = b + 1;
             if (ALT && a.mode == RTG_INTEGRATOR_DIRECT_MIS && b == 1) {
@@ -2033,6 +2036,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         a.mode = h->integrator;
         a.pm = h->pixel_major;
         a.cam = h->cam;
+        a.lean = RTG_GEN_LEAN && !use_packet;
         HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), cs));
         timed_begin(h, cs, k);
         hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, cs, a, pb);
@@ -2051,8 +2055,9 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                 LAUNCH_OK("k_shade");
                 timed_end(h, cs, k); kinds.push_back(2); ++k;
             }
-            io.queue = pb.q[b & 1];
-            io.ray_o = pb.ray_o;
+            io.queue = (a.lean && b == 0) ? nullptr : pb.q[b & 1];
+            io.ray_o = (a.lean && b == 0) ? nullptr : pb.ray_o;
+            io.cam_o = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f);
             io.ray_d = pb.ray_d;
             io.count = b < maxb ? &pb.ctr[b].n_ext : nullptr;
             io.hits = pb.hits;
