@@ -124,8 +124,8 @@ def main():
         rt.clear()
         rt.render(a.spp, tiles=tiles, first_sample=0)
         if world > 1:
+            import torch
             if backend == "nccl":
-                import torch
                 torch.cuda.synchronize()  # the previous step's reduce is done with film_t
                 rt.copy_film_to(film_t.data_ptr())
             else:
