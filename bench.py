@@ -220,8 +220,12 @@ def main():
     b_sray = 32.0 * s_boxes_per_ray + 36.0 * s_tris_per_ray + 48.0
     # time and rays both summed over ranks and launches
     achieved_gbs = (b_ray * ext_rays + b_sray * shadow_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
+    # the PMC summary is per launch of the default workload (C3, 64 spp, one rank): other workloads
+    # (configs, shards, N > 1 ranks) have other launch sizes and report no measured traffic
     traffic = None
-    if os.path.exists(PMC_SUMMARY):
+    profiled = (a.config == "C3" and world == 1 and a.shard_of <= 1 and a.spp == 64 and a.tris == 1_000_000
+                and (a.width, a.height) == (1024, 1024) and a.max_depth == 4)
+    if profiled and os.path.exists(PMC_SUMMARY):
         try:
             traffic = json.load(open(PMC_SUMMARY)).get("extend_hbm_bytes_per_launch")
         except Exception:
