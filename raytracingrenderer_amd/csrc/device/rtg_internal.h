@@ -78,7 +78,7 @@ using namespace rtgd;
 #define RTG_SHADE_SORT 0    // 1: k_shade partitions each block's paths into misses and hits first (C3: no change)
 #endif
 #ifndef RTG_SHADE_WAVES
-#define RTG_SHADE_WAVES 4                // min waves per SIMD for k_shade (register budget)
+#define RTG_SHADE_WAVES 5                // min waves per SIMD for k_shade (96 VGPRs, no spills)
 #endif
 
 // Work counters of one bounce. Every field sits in its own 128-B line (RTG_CTR_PAD): the
