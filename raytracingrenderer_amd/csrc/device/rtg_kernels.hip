@@ -1982,6 +1982,18 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     // computeDirectMIS keeps two scratch planes of per-path state in contrib planes 2 and 3
     const int planes = h->integrator == RTG_INTEGRATOR_DIRECT_MIS ? std::max(maxb, 4) : maxb;
     uint32_t ns_chunk = std::max<uint32_t>(1, std::min<uint32_t>(n_samples, h->max_paths / std::max(1u, h->npix)));
+    {
+        // path state of a chunk takes at most half the free HBM (buffers held now count as free)
+        size_t freeb = 0, totalb = 0;
+        if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
+            auto path_bytes = [](int pl) { return (size_t)152 + (size_t)16 * (size_t)pl; };
+            size_t held = 0;
+            for (int i = 0; i < 2; ++i) held += h->cap_P[i] * path_bytes(h->cap_maxb[i]);
+            const size_t budget = (freeb + held) / 2 / (h->pipes >= 2 ? 2 : 1);
+            const size_t max_ns = budget / path_bytes(planes) / std::max<size_t>(1, h->npix);
+            ns_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(ns_chunk, max_ns));
+        }
+    }
     // Two chunk pipelines: the samples are split into (at least) two chunks that alternate between
     // the caller's stream and stream2, so that one chunk's trace drain tails (a few hundred us per
     // launch: the longest rays' dependent fetch chains) overlap the other chunk's work. The film
