@@ -25,7 +25,7 @@ using namespace rtgd;
 #define RTG_DRAIN_LEAF 1    // once the queue is empty, run the leaf phase whenever a lane has parked a
 #endif                      //     leaf (the drain is latency-bound: lanes should not wait for each other)
 #ifndef RTG_REFILL
-#define RTG_REFILL 16       // refill idle lanes once at least this many are idle (the setup code then
+#define RTG_REFILL 12       // refill idle lanes once at least this many are idle (the setup code then
 #endif                      // runs with more lanes per execution)
 #ifndef RTG_TRACE_WPE
 #define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel
