@@ -158,7 +158,10 @@ int  rtg_set_integrator(rtg_handle* h, int integrator);
 /* Add samples [first_sample, first_sample+n_samples) of every pixel in the listed 32x32 tiles
  * (tile id = ty*tilesX + tx, RTBase TILE_SIZE=32; tile_ids=NULL = all tiles) to the film, in
  * sample order per pixel. Equivalent to n_samples calls of RayTracer::render() with the
- * deterministic sampler. Synchronous unless rtg_render_async is used. */
+ * deterministic sampler. Synchronous unless rtg_render_async is used.
+ * Sample indices must stay below RTG_MAX_SAMPLES_PER_KEY: the PCG stream of (pixel, sample) is
+ * keyed seq = pixel << 16 | sample; more samples take another seed. */
+#define RTG_MAX_SAMPLES_PER_KEY 65536u
 int  rtg_render(rtg_handle* h, uint32_t first_sample, uint32_t n_samples, uint64_t seed,
                 const uint32_t* tile_ids, uint32_t n_tiles);
 int  rtg_render_async(rtg_handle* h, uint32_t first_sample, uint32_t n_samples, uint64_t seed,
@@ -172,7 +175,10 @@ int  rtg_synchronize(rtg_handle* h);
  * min_samples) samples of each pixel of the tile (indices first_sample + init_samples ...) and adds
  * their mean to the film (sampleTileWithWeight, :640-672). The reference constants are INIT_SAMPLES
  * 2, MAX_SAMPLES 10240, MIN_SAMPLES 1 (Renderer.h:20-23). tile_samples (optional, tilesX*tilesY)
- * receives each tile's pass-2 sample count. */
+ * receives each tile's pass-2 sample count. first_sample + init_samples + the largest tile count
+ * must be <= RTG_MAX_SAMPLES_PER_KEY (checked before the film is touched: RTG_ERR_ARG). Pass 2 is
+ * staged and published only when every tile group succeeded, so a failed call leaves the film and
+ * SPP as they were. */
 /* RayTracer::lightTracer (Renderer.h:221-326): each frame traces width*height light paths (path i
  * of frame f draws from the PCG stream keyed (seed, i, f)), connects every non-specular vertex to
  * the camera (connectToCamera: projectOntoCamera, importance W_e = 1/(Afilm cos^4), visibility)

@@ -36,6 +36,8 @@ def lib(flavour="rtm"):
         L.or_camera_project.argtypes = [vp, f32p, C.c_uint32, f32p]
         L.or_light_emit.argtypes = [vp, C.c_int, f32p, f32p]
         L.or_trace_paths.argtypes = [vp, u32p, u32p, C.c_uint32, C.c_uint64, f32p]
+        L.or_path_events.restype = C.c_int
+        L.or_path_events.argtypes = [vp, C.c_uint32, C.c_uint32, C.c_uint64, f32p, C.c_int, f32p]
         L.or_trace_closest.argtypes = [vp, f32p, C.c_uint32, f32p]
         L.or_trace_visible.argtypes = [vp, f32p, C.c_uint32, i32p]
         L.or_camera_rays.argtypes = [vp, u32p, C.c_uint32, f32p]
@@ -125,6 +127,19 @@ class Oracle:
         out = np.zeros((len(p), 3), np.float32)
         self.L.or_trace_paths(self.h, _p(p, C.c_uint32), _p(s, C.c_uint32), len(p), seed, _p(out, C.c_float))
         return out
+
+    EVENT_KINDS = {1: "closest hit (id, t, alpha, beta)", 2: "light sample (index, point/direction)",
+                   3: "shadow ray (visible, maxT)", 4: "russian roulette (draw, probability, depth)",
+                   5: "BSDF sample (wi, pdf)"}
+
+    def path_events(self, pixel, sample, seed=1234, cap=256):
+        """Event list of one path (or_path_events): (events[n, 5], radiance[3])."""
+        ev = np.zeros((cap, 5), np.float32)
+        L = np.zeros(3, np.float32)
+        n = self.L.or_path_events(self.h, pixel, sample, seed, _p(ev, C.c_float), cap, _p(L, C.c_float))
+        if n < 0:
+            raise RuntimeError("or_path_events failed")
+        return ev[: min(n, cap)], L
 
     def trace_closest(self, rays):
         r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)

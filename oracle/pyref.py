@@ -128,3 +128,13 @@ def load_texture(path, cap=1 << 24):
     wh = np.zeros(2, np.int32)
     n = lib().ref_load_texture(os.fsencode(path), _p(out), cap, _p(wh))
     return out[: n * 3].reshape(wh[1], wh[0], 3)
+
+
+def tonemap(film_sum, spp, exposure=1.0):
+    """Film::tonemap (Imaging.h:233-242) of every pixel, from the reference's own class."""
+    f = np.ascontiguousarray(film_sum, np.float32)
+    out = np.zeros(f.shape[:2] + (3,), np.uint8)
+    L = lib()
+    L.ref_tonemap.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_float, C.c_void_p]
+    L.ref_tonemap(f.shape[1], f.shape[0], f.ctypes.data, spp, C.c_float(exposure), out.ctypes.data)
+    return out

@@ -388,6 +388,19 @@ int ref_save_hdr(const char* path, int w, int h, const float* sum, int spp) {
     return 0;
 }
 
+// Film::tonemap (Imaging.h:233-242) of every pixel of a w*h film sum: out w*h*3 bytes.
+void ref_tonemap(int w, int h, const float* sum, int spp, float exposure, unsigned char* out) {
+    Film f;
+    f.init(w, h, new BoxFilter());
+    memcpy(f.film, sum, (size_t)w * h * 12);
+    f.SPP = spp;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            unsigned char* o = out + ((size_t)y * w + x) * 3;
+            f.tonemap(x, y, o[0], o[1], o[2], exposure);
+        }
+}
+
 // stbi_loadf / stbi_load as Texture::load sees them.
 int ref_load_texture(const char* path, float* out, int cap, int* wh) {
     Texture t;

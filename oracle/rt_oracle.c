@@ -148,6 +148,19 @@ typedef struct {
     uint64_t ext_rays, shadow_rays, nodes, tris;
 } Counts;
 
+/* Optional per-path event log (or_path_events): the first differing event of two builds' paths
+ * names where a divergent pixel's paths part ways. Thread-local, off unless set. */
+typedef struct { float* ev; int n, cap; } EvLog;
+static __thread EvLog* g_ev;
+static void ev_push(float kind, float a, float b, float c, float d) {
+    if (!g_ev) return;
+    if (g_ev->n < g_ev->cap) {
+        float* e = g_ev->ev + (size_t)g_ev->n * 5;
+        e[0] = kind; e[1] = a; e[2] = b; e[3] = c; e[4] = d;
+    }
+    g_ev->n++;
+}
+
 typedef struct { V3 o, dir, inv; } Ray;
 static Ray ray_make(V3 o, V3 d) { Ray r; r.o = o; r.dir = d; r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); return r; }
 
@@ -231,6 +244,7 @@ static Isect scene_traverse(const struct or_scene* s, const Ray* r, Counts* c) {
     is.alpha = is.beta = is.gamma = 0;
     if (c) c->ext_rays++;
     traverse(s, 0, r, &is, c);
+    ev_push(1, (float)is.id, is.t, is.alpha, is.beta); /* closest hit (id -1: miss) */
     return is;
 }
 
@@ -241,7 +255,9 @@ static int scene_visible(const struct or_scene* s, V3 p1, V3 p2, Counts* c) {
     dir = vnorm(dir);
     Ray r = ray_make(vadd(p1, vmuls(dir, O_EPS)), dir);
     if (c) c->shadow_rays++;
-    return traverse_visible(s, 0, &r, maxT, c);
+    int vis = traverse_visible(s, 0, &r, maxT, c);
+    ev_push(3, (float)vis, maxT, 0, 0); /* shadow ray */
+    return vis;
 }
 
 /* Texture::sample (Imaging.h:72-94) */
@@ -352,6 +368,7 @@ static Col compute_direct(const struct or_scene* s, const Shading* sd, Pcg* smp,
         float gamma = 1.0f - (alpha + beta);
         float pdf = 1.0f / T->area;
         V3 p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+        ev_push(2, (float)li, p.x, p.y, p.z); /* area light sample point */
         const float* e = s->mat[T->mat].emission;
         Col emitted = col(e[0], e[1], e[2]);
         V3 wi = vsub(p, sd->x);
@@ -367,6 +384,7 @@ static Col compute_direct(const struct or_scene* s, const Shading* sd, Pcg* smp,
         float q2 = pcg_next(smp);
         float q1 = pcg_next(smp);
         V3 wi = uniform_sample_sphere(q1, q2);
+        ev_push(2, (float)li, wi.x, wi.y, wi.z); /* environment sample direction */
         float pdf = (float)(1.0f / (4.0f * O_PI));
         Col emitted = env_eval(s, wi);
         float G = win_max(vdot(wi, sd->sN), 0.0f);
@@ -449,6 +467,7 @@ static Col compute_direct_mis(const struct or_scene* s, const Shading* sd, Pcg* 
         float gamma = 1.0f - (alpha + beta);
         pdf = 1.0f / T->area;
         V3 p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+        ev_push(2, (float)li, p.x, p.y, p.z); /* area light sample point */
         const float* e = s->mat[T->mat].emission;
         Col emitted = col(e[0], e[1], e[2]);
         V3 wi = vsub(p, sd->x);
@@ -515,11 +534,14 @@ static Col path_trace(const struct or_scene* s, Ray* r, Col* thr, int depth, Pcg
         Col direct = cmul(*thr, compute_direct(s, &sd, smp, c));
         if (depth > s->max_depth) return direct;
         float rrp = win_min(clum(*thr), 0.9f);
-        if (pcg_next(smp) < rrp) *thr = cdivs(*thr, rrp);
+        float q = pcg_next(smp);
+        ev_push(4, q, rrp, (float)depth, 0); /* Russian roulette */
+        if (q < rrp) *thr = cdivs(*thr, rrp);
         else return direct;
         Col ind;
         float pdf;
         V3 wi = bsdf_sample(s, &sd, smp, &ind, &pdf);
+        ev_push(5, wi.x, wi.y, wi.z, pdf); /* BSDF sample */
         if (is_spec(sd.bsdf)) *thr = cdivs(cmul(*thr, ind), pdf);
         else *thr = cdivs(cmuls(cmul(*thr, ind), fabsf(vdot(wi, sd.sN))), pdf);
         *r = ray_make(vadd(sd.x, vmuls(wi, O_EPS)), wi);
@@ -687,6 +709,20 @@ int or_trace_paths(or_scene* s, const uint32_t* pixels, const uint32_t* samples,
         out[i * 3] = L.r; out[i * 3 + 1] = L.g; out[i * 3 + 2] = L.b;
     }
     return 0;
+}
+
+/* Event log of one path (pixel, sample): up to cap events of 5 floats {kind, a, b, c, d}:
+ * 1 closest hit {id, t, alpha, beta}, 2 light sample {index, point or direction}, 3 shadow ray
+ * {visible, maxT}, 4 Russian roulette {draw, probability, depth}, 5 BSDF sample {wi, pdf}.
+ * Returns the number of events (may exceed cap); radiance goes to L (3 floats). */
+int or_path_events(or_scene* s, uint32_t pixel, uint32_t sample, uint64_t seed, float* ev, int cap, float* L) {
+    if (!s || s->nlight <= 0) return -1;
+    EvLog log = {ev, 0, cap};
+    g_ev = &log;
+    Col c = pixel_sample(s, pixel, sample, seed, NULL);
+    g_ev = NULL;
+    if (L) { L[0] = c.r; L[1] = c.g; L[2] = c.b; }
+    return log.n;
 }
 
 /* RayTracer::render over tiles with a thread pool: for each sample (frame) in order, the

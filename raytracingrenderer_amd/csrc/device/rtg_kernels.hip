@@ -2244,6 +2244,17 @@ int rtg_render_adaptive(rtg_handle* h, uint32_t first, uint64_t seed, uint32_t i
         if (tile_samples) tile_samples[t] = (uint32_t)smp;
     }
     std::sort(cnt.begin(), cnt.end());
+    // every pass-2 sample index must stay inside the PCG key (seq = pixel << 16 | sample): checked
+    // before the film is touched
+    if (!cnt.empty() && (uint64_t)first + init_samples + cnt.back().first > RTG_MAX_SAMPLES_PER_KEY) {
+        g_err = "rtg_render_adaptive: first_sample + init_samples + max tile count exceeds 65536";
+        return fail(RTG_ERR_ARG);
+    }
+    // pass 2 folds into a staged copy of the film, published only when every group succeeded
+    float* d_acc = nullptr;
+    if (hipMalloc((void**)&d_acc, nf * sizeof(float)) != hipSuccess) { g_err = "rtg_render_adaptive: out of memory"; return fail(RTG_ERR_HIP); }
+    auto fail2 = [&](int rc) { (void)hipFree(d_acc); return fail(rc); };
+    if (hipMemcpyAsync(d_acc, d_keep, nf * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess) return fail2(RTG_ERR_HIP);
     for (size_t i = 0; i < cnt.size();) {
         size_t j = i;
         std::vector<uint32_t> group;
@@ -2252,15 +2263,17 @@ int rtg_render_adaptive(rtg_handle* h, uint32_t first, uint64_t seed, uint32_t i
         i = j;
         if (n == 0) continue;
         h->d_film = d_tmp;
-        if (hipMemsetAsync(d_tmp, 0, nf * sizeof(float), st) != hipSuccess) return fail(RTG_ERR_HIP);
-        if ((rc = render_impl(h, first + init_samples, n, seed, group.data(), (uint32_t)group.size(), st))) return fail(rc);
+        if (hipMemsetAsync(d_tmp, 0, nf * sizeof(float), st) != hipSuccess) return fail2(RTG_ERR_HIP);
+        if ((rc = render_impl(h, first + init_samples, n, seed, group.data(), (uint32_t)group.size(), st))) return fail2(rc);
         h->d_film = d_keep;
         hipLaunchKernelGGL(k_fold_mean, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, h->d_pix, h->npix,
-                           (const float*)d_tmp, (float)n, d_keep);
-        if (hipGetLastError() != hipSuccess) { g_err = "launch k_fold_mean failed"; return fail(RTG_ERR_HIP); }
+                           (const float*)d_tmp, (float)n, d_acc);
+        if (hipGetLastError() != hipSuccess) { g_err = "launch k_fold_mean failed"; return fail2(RTG_ERR_HIP); }
     }
     h->d_film = d_keep;
+    if (hipMemcpyAsync(d_keep, d_acc, nf * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess) return fail2(RTG_ERR_HIP);
     HIPOK(hipStreamSynchronize(st));
+    (void)hipFree(d_acc);
     (void)hipFree(d_tmp);
     h->spp = spp0 + 1;  // render(): film->incrementSPP() once per frame
     return RTG_OK;

@@ -27,10 +27,24 @@ def reduce_film(film_tensor, dist, dst=0):
 
 
 def render_sharded(rt, n_samples, rank, world, dist=None, film_tensor=None, first_sample=0):
-    """Render this rank's tiles with RayTracer `rt`, then reduce to rank 0 (if world > 1)."""
+    """Render this rank's tiles with RayTracer `rt`, then reduce the films to rank 0.
+
+    world > 1: film_tensor (torch float32 HxWx3) receives this rank's film and, on rank 0, the sum;
+    a CUDA tensor is filled on the device (RCCL), a CPU tensor through host memory (gloo). Returns
+    film_tensor. world == 1: returns film_tensor filled the same way if given, else the film as a
+    numpy array."""
     tiles = tiles_for_rank(rt.width, rt.height, rank, world)
     rt.render(n_samples, tiles=tiles, first_sample=first_sample)
-    if world > 1:
+    if film_tensor is None:
+        if world > 1:
+            raise ValueError("render_sharded: world > 1 needs a film_tensor to reduce into")
+        return rt.film()[0]
+    if film_tensor.is_cuda:
         rt.copy_film_to(film_tensor.data_ptr())
+        rt.synchronize()
+    else:
+        import torch
+        film_tensor.copy_(torch.from_numpy(rt.film()[0]))
+    if world > 1:
         reduce_film(film_tensor, dist)
     return film_tensor

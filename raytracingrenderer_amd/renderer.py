@@ -225,11 +225,16 @@ class RayTracer:
     def adaptiveRender(self, init_samples=2, max_samples=10240, min_samples=1, first_sample=None):
         """RayTracer::adaptiveRender (Renderer.h:583-749): one frame whose per-tile sample counts
         follow the tiles' variance after init_samples samples. Returns the per-tile counts. The frame
-        draws sample indices first_sample ... first_sample + init_samples + max(count) - 1 (default:
-        frame f starts at f * (init_samples + max_samples))."""
-        first = self.getSPP() * (init_samples + max_samples) if first_sample is None else first_sample
+        draws sample indices first_sample ... first_sample + init_samples + max(count) - 1 of the
+        PCG streams keyed by `seed` (limit: RTG_MAX_SAMPLES_PER_KEY = 65536). Default (first_sample
+        None): frame f = getSPP() draws indices 0 ... of its own seed, seed + f * 0x9E3779B97F4A7C15
+        (mod 2^64), so any number of frames stays inside the key space."""
+        if first_sample is None:
+            first, seed = 0, (self.seed + self.getSPP() * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+        else:
+            first, seed = first_sample, self.seed
         counts = np.zeros(self.tiles_x * self.tiles_y, np.uint32)
-        _check(self._lib.rtg_render_adaptive(self._h, first, self.seed, init_samples, max_samples, min_samples,
+        _check(self._lib.rtg_render_adaptive(self._h, first, seed, init_samples, max_samples, min_samples,
                                              N.ptr(counts, C.c_uint32)), self._lib.rtg_last_error)
         return counts
 

@@ -121,6 +121,8 @@ def main():
     np.savez_compressed(os.path.join(GOLD, "rgbe_kat.npz"), film=film, spp=3,
                         hdr=np.frombuffer(open("/tmp/rtg_golden_film.hdr", "rb").read(), np.uint8))
     light_fixtures()
+    synth1m_digests()
+    tonemap_fixture()
     print("golden fixtures written to", GOLD)
 
 
@@ -148,8 +150,41 @@ def light_fixtures():
     np.savez_compressed(os.path.join(GOLD, "light_kat.npz"), **out)
 
 
+def synth1m_digests():
+    """Config C3's scene (1M splitmix64 triangles, seed 20251015, 1024^2) through the reference loader
+    and Scene::build (Geometry.h:325-398): digests of positions (the std::sort permutation), BVH
+    nodes, lights and camera -> scene_digests.json["synth1m"]."""
+    path = "/tmp/rtg_golden_synth1m"
+    write_synthetic_scene(path, n_tris=1_000_000, seed=20251015, width=1024, height=1024)
+    r = pyref.RefScene(path, 0, 0, False)
+    d = r.export()
+    dg = json.load(open(os.path.join(GOLD, "scene_digests.json")))
+    dg["synth1m"] = {k: digest(d[k]) for k in ARRAYS}
+    dg["synth1m"].update(n_tris=r.ntri, n_nodes=r.nnode, n_lights=r.nlight, width=r.W, height=r.H,
+                         mat_info=digest(d["mat_info"][:, :2]), mat_f=digest(d["mat_f"]))
+    json.dump(dg, open(os.path.join(GOLD, "scene_digests.json"), "w"), indent=1, sort_keys=True)
+
+
+def tonemap_fixture():
+    """Film::tonemap (Imaging.h:233-242) of the reference's own Film class on a random film with
+    negative, zero, tiny, saturating and non-finite values, at two exposures -> tonemap_kat.npz."""
+    rng = np.random.default_rng(8)
+    film = rng.gamma(0.7, 2.0, (17, 23, 3)).astype(np.float32)
+    film[0, :6] = [[-1.0, 0.0, 1e9], [np.inf, -np.inf, np.nan], [1e-30, 1e-7, 3.0],
+                   [2.99, 3.01, 2.2], [0.5, 0.25, 0.125], [-0.0, 7.5, 1e38]]
+    out = {"film": film, "spp": np.int32(3)}
+    for k, e in enumerate((1.0, 0.37)):
+        out["exposure%d" % k] = np.float32(e)
+        out["rgb%d" % k] = pyref.tonemap(film, 3, e)
+    np.savez_compressed(os.path.join(GOLD, "tonemap_kat.npz"), **out)
+
+
 if __name__ == "__main__":
     if "--light-only" in sys.argv:
         light_fixtures()
+    elif "--synth1m" in sys.argv:
+        synth1m_digests()
+    elif "--tonemap" in sys.argv:
+        tonemap_fixture()
     else:
         main()
