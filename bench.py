@@ -106,7 +106,8 @@ def main():
         write_synthetic_scene(work, n_tris=a.tris, seed=a.seed, width=a.width, height=a.height)
         scene = loadScene(work)
     else:
-        scene = loadScene(scene_dir(cfg["scene"]), width=a.width, height=a.height,
+        work = scene_dir(cfg["scene"])
+        scene = loadScene(work, width=a.width, height=a.height,
                           skip_missing=cfg.get("skip_missing", False), envmap=cfg.get("envmap"))
     setup_s = time.time() - t0
     rt = RayTracer(scene, device=local, max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
@@ -233,7 +234,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(scene, a)
+        cpu = cpu_baseline(scene, a, work)
 
     if rank == 0:
         out = {
@@ -300,33 +301,85 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(scene, a):
-    """The C oracle's tile renderer (the reference algorithm: unordered DFS, no culling) on the
-    host cores, bounded sample: whole 1-spp frames of the same scene until ~cpu_seconds pass."""
+def host_cores():
+    """Host cores this process may use: the CPU affinity set, capped by a cgroup CPU quota and by
+    OMP_NUM_THREADS (the GPU box sets it to the job's CPU share; os.cpu_count() there shows the
+    whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     try:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(float(quota) / float(period))))
+    except Exception:
+        pass
+    try:
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        pass
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(scene, a, scene_path=None):
+    """The reference CPU tile renderer timed on this host's cores, on a bounded sample: whole 1-spp
+    frames of the same scene until ~cpu_seconds pass.
+
+    kind "reference": oracle/_ref's ref_render -- RTBase's own classes (BVHNode::traverse,
+    Scene::visible, BSDFs, lights, Camera, Film) compiled from the reference headers, with the
+    unbuildable Renderer.h's pathTrace/computeDirect/tile pool restated on top; its film is
+    bit-identical to the oracle's and reproduces the survey's C1 md5. It loads the scene with the
+    reference's own loader and builds the reference BVH (outside the timing).
+    kind "port": oracle/rt_oracle.c's tile renderer, when oracle/_ref was not built."""
+    threads = host_cores()
+    base = {"cores": threads, "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count()}
+    try:
+        from oracle import pyref
         from oracle.pyoracle import Oracle
     except Exception as e:  # pragma: no cover
-        return {"error": "oracle unavailable: %s" % e}
-    threads = min(16, os.cpu_count() or 1)
-    o = Oracle(scene, max_depth=a.max_depth, flavour="libm")
-    rays = paths = 0
-    frames = 0
-    t0 = time.perf_counter()
+        return dict(base, error="oracle unavailable: %s" % e)
+    if scene_path is not None and pyref.available():
+        cfg = CONFIGS[a.config]
+        t0 = time.perf_counter()
+        r = pyref.RefScene(scene_path, a.width, a.height, cfg.get("skip_missing", False), cfg.get("envmap"))
+        load_s = time.perf_counter() - t0
+
+        def frame(f, film):
+            return r.render(1, first=f, seed=1234, max_depth=a.max_depth, threads=threads, film=film)
+        kind, what = "reference", ("oracle/_ref ref_render: RTBase's own classes (BVHNode::traverse, BSDFs, lights, "
+                                   "Film) with Renderer.h's pathTrace/tile pool restated, %d std::threads" % threads)
+    else:
+        o = Oracle(scene, max_depth=a.max_depth, flavour="libm")
+        load_s = 0.0
+
+        def frame(f, film):
+            fl, c = o.render(1, first=f, seed=1234, threads=threads, film=film, count=True)
+            return fl, [c[0], c[1], c[2]]
+        kind, what = "port", "oracle/rt_oracle.c tile renderer (reference DFS traversal, no culling), %d threads" % threads
+    rays = paths = frames = 0
     film = np.zeros((scene.height, scene.width, 3), np.float32)
+    t0 = time.perf_counter()
     while frames < 8:
-        _, c = o.render(1, first=frames, seed=1234, threads=threads, film=film, count=True)
+        _, c = frame(frames, film)
         paths += int(c[0])
-        rays += int(c[1] + c[2])
+        rays += int(c[1]) + int(c[2])
         frames += 1
         if time.perf_counter() - t0 > a.cpu_seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mray/s", "cores": threads, "kind": "port",
-            "sample": "%d full %dx%d frame(s) at 1 spp of the same scene (%d paths, %d rays) in %.1f s; "
-                      "oracle/rt_oracle.c tile renderer (reference DFS traversal, no culling), %d threads"
-                      % (frames, scene.width, scene.height, paths, rays, dt, threads),
-            "ms_per_frame": round(dt * 1e3 / frames, 1)}
+    return dict(base, value=round(rays / dt / 1e6, 3), unit="Mray/s", kind=kind,
+                sample="%d full %dx%d frame(s) at 1 spp of the same scene, MAX_DEPTH %d (%d paths, %d rays) in "
+                       "%.1f s; %s; glibc math" % (frames, scene.width, scene.height, a.max_depth, paths, rays, dt, what),
+                ms_per_frame=round(dt * 1e3 / frames, 1), mpaths_per_s=round(paths / dt / 1e6, 3),
+                load_and_bvh_s=round(load_s, 2))
 
 
 if __name__ == "__main__":

@@ -47,6 +47,20 @@ class RefScene:
         self.L.ref_counts(C.c_void_p(self.h), _p(c))
         self.ntri, self.nnode, self.nlight, self.nmat, self.ntex, self.env_tex, self.W, self.H = c.tolist()
 
+    def render(self, n_samples, first=0, seed=1234, max_depth=4, threads=8, film=None, count=False):
+        """ref_render: RayTracer::render x n_samples on the reference's own classes (tile pool of
+        `threads` std::threads, deterministic sampler). Returns (film sum, counts[paths, closest,
+        shadow])."""
+        if film is None:
+            film = np.zeros((self.H, self.W, 3), np.float32)
+        counts = np.zeros(3, np.uint64)
+        L = self.L
+        L.ref_render.restype = C.c_int
+        L.ref_render.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.c_void_p,
+                                 C.c_void_p]
+        L.ref_render(self.h, first, n_samples, seed, max_depth, threads, film.ctypes.data, counts.ctypes.data)
+        return film, counts
+
     def export(self):
         n, m = self.ntri, self.nnode
         d = {"positions": np.zeros((n, 3, 3), np.float32), "normals": np.zeros((n, 3, 3), np.float32),

@@ -9,14 +9,20 @@
 //
 // NOT compilable here: Renderer.h and SceneLoader.h include the Windows/D3D11-only
 // GamesEngineeringBase.h (windows.h, d3d11.h, XAudio2...). So loadScene's ~60-line glue
-// (SceneLoader.h:104-291) is restated below using the reference classes, and pathTrace /
-// computeDirect are not exercised here (the integrator is pinned by the survey's known answer).
+// (SceneLoader.h:104-291) is restated below using the reference classes, and so are the few lines
+// of RayTracer::pathTrace / computeDirect / renderTile / pathTracerTileBased (Renderer.h:328-473,
+// 795-853) in ref_render: every call they make (Scene::traverse, calculateShadingData,
+// sampleLight, Light::sample, BSDF::sample/evaluate, Scene::visible, Camera::generateRay,
+// Film::splat) is the reference's own compiled code. ref_render is a second, independent
+// film-level pin of the C oracle and the "reference" CPU baseline of bench.py.
 #include "GEMLoader.h"
 #include "Scene.h"
 
 #include <sys/stat.h>
 
+#include <atomic>
 #include <cstdint>
+#include <thread>
 #include <map>
 #include <string>
 #include <vector>
@@ -29,6 +35,87 @@ struct ScriptSampler : Sampler {
     ScriptSampler(const float* vals, int count) : v(vals), n(count) {}
     float next() override { return i < n ? v[i++] : 0.5f; }
 };
+
+// PCG32 keyed by seq = pixel << 16 | sample, next() = (pcg32 >> 8) * 2^-24.
+struct PcgSampler : Sampler {
+    uint64_t state = 0, inc = 1;
+    PcgSampler(uint64_t seed, uint64_t seq) {
+        inc = (seq << 1u) | 1u;
+        step();
+        state += seed;
+        step();
+    }
+    uint32_t step() {
+        uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        uint32_t x = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (x >> rot) | (x << ((0u - rot) & 31u));
+    }
+    float next() override { return (float)(step() >> 8) * (1.0f / 16777216.0f); }
+};
+
+// windows.h min/max macros, as Renderer.h sees them
+template <class T> inline T win_min(T a, T b) { return a < b ? a : b; }
+template <class T> inline T win_max(T a, T b) { return a > b ? a : b; }
+
+struct RayCount { uint64_t ext = 0, shadow = 0; };
+
+// RayTracer::computeDirect (Renderer.h:423-473) on the reference classes
+Colour ref_compute_direct(Scene* scene, ShadingData shadingData, Sampler& sampler, RayCount& rc) {
+    if (shadingData.bsdf->isPureSpecular() == true) return Colour(0.0f, 0.0f, 0.0f);
+    float pmf;
+    Light* light = scene->sampleLight(sampler, pmf);
+    float pdf;
+    Colour emitted;
+    Vec3 p = light->sample(shadingData, sampler, emitted, pdf);
+    if (light->isArea()) {
+        Vec3 wi = p - shadingData.x;
+        float l = wi.lengthSq();
+        wi = wi.normalize();
+        float g = (win_max(Dot(wi, shadingData.sNormal), 0.0f) * win_max(-Dot(wi, light->normal(shadingData, wi)), 0.0f)) / l;
+        if (g > 0) {
+            rc.shadow++;
+            if (scene->visible(shadingData.x, p)) return shadingData.bsdf->evaluate(shadingData, wi) * emitted * g / (pmf * pdf);
+        }
+    } else {
+        Vec3 wi = p;
+        float g = win_max(Dot(wi, shadingData.sNormal), 0.0f);
+        if (g > 0) {
+            rc.shadow++;
+            if (scene->visible(shadingData.x, shadingData.x + (p * 10000.0f)))
+                return shadingData.bsdf->evaluate(shadingData, wi) * emitted * g / (pmf * pdf);
+        }
+    }
+    return Colour(0.0f, 0.0f, 0.0f);
+}
+
+// RayTracer::pathTrace (Renderer.h:328-392) with MAX_DEPTH as a parameter
+Colour ref_path_trace(Scene* scene, Ray& r, Colour& thr, int depth, int max_depth, Sampler& sampler, bool canHitLight,
+                      RayCount& rc) {
+    rc.ext++;
+    IntersectionData intersection = scene->traverse(r);
+    ShadingData shadingData = scene->calculateShadingData(intersection, r);
+    if (shadingData.t < FLT_MAX) {
+        if (shadingData.bsdf->isLight()) {
+            if (canHitLight == true) return thr * shadingData.bsdf->emit(shadingData, shadingData.wo);
+            return Colour(0.0f, 0.0f, 0.0f);
+        }
+        Colour direct = thr * ref_compute_direct(scene, shadingData, sampler, rc);
+        if (depth > max_depth) return direct;
+        float rrp = win_min(thr.Lum(), 0.9f);
+        if (sampler.next() < rrp) thr = thr / rrp;
+        else return direct;
+        Colour indirect;
+        float pdf;
+        Vec3 wi = shadingData.bsdf->sample(shadingData, sampler, indirect, pdf);
+        if (shadingData.bsdf->isPureSpecular()) thr = thr * indirect / pdf;
+        else thr = thr * indirect * fabsf(Dot(wi, shadingData.sNormal)) / pdf;
+        r.init(shadingData.x + (wi * EPSILON), wi);
+        return (direct + ref_path_trace(scene, r, thr, depth + 1, max_depth, sampler, shadingData.bsdf->isPureSpecular(), rc));
+    }
+    return scene->background->evaluate(r.dir);
+}
 
 bool exists(const std::string& p) {
     struct stat st;
@@ -385,6 +472,54 @@ int ref_save_hdr(const char* path, int w, int h, const float* sum, int spp) {
     memcpy(f.film, sum, (size_t)w * h * 12);
     f.SPP = spp;
     f.save(path);
+    return 0;
+}
+
+// RayTracer::render x n_samples (Renderer.h:876-885 -> pathTracerTileBased / getTileID /
+// renderTile, :795-853): per frame, `threads` std::threads pop 32x32 tiles from a shared counter
+// and splat every pixel's pathTrace radiance into the reference's Film (box filter). The film sum
+// (w*h*3, in/out) and the deterministic sampler replace MTRandom. counts (optional, 3): paths,
+// closest-hit rays, shadow rays.
+int ref_render(void* h, uint32_t first, uint32_t n_samples, uint64_t seed, int max_depth, int threads, float* sum,
+               uint64_t* counts) {
+    RefScene* rs = (RefScene*)h;
+    Scene* scene = rs->scene;
+    const int W = (int)scene->camera.width, H = (int)scene->camera.height, TS = 32;
+    Film film;
+    film.init(W, H, new BoxFilter());
+    memcpy(film.film, sum, (size_t)W * H * 12);
+    const int tx = (W + TS - 1) / TS, ty = (H + TS - 1) / TS;
+    if (threads < 1) threads = 1;
+    std::vector<RayCount> rcs(threads);
+    for (uint32_t smp = first; smp < first + n_samples; ++smp) {
+        std::atomic<int> next(0);
+        auto worker = [&](int tid) {
+            for (;;) {
+                int t = next.fetch_add(1);
+                if (t >= tx * ty) break;
+                int x0 = (t % tx) * TS, y0 = (t / tx) * TS;
+                int x1 = win_min(x0 + TS, W), y1 = win_min(y0 + TS, H);
+                for (int y = y0; y < y1; y++)
+                    for (int x = x0; x < x1; x++) {
+                        float px = x + 0.5f, py = y + 0.5f;
+                        PcgSampler sampler(seed, ((uint64_t)(y * W + x) << 16) | smp);
+                        Ray ray = scene->camera.generateRay(px, py);
+                        Colour thr(1.0f, 1.0f, 1.0f);
+                        Colour col = ref_path_trace(scene, ray, thr, 0, max_depth, sampler, true, rcs[tid]);
+                        film.splat(px, py, col);
+                    }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int i = 0; i < threads; i++) pool.emplace_back(worker, i);
+        for (auto& t : pool) t.join();
+    }
+    memcpy(sum, film.film, (size_t)W * H * 12);
+    if (counts) {
+        counts[0] = (uint64_t)W * H * n_samples;
+        counts[1] = counts[2] = 0;
+        for (auto& c : rcs) { counts[1] += c.ext; counts[2] += c.shadow; }
+    }
     return 0;
 }
 

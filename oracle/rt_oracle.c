@@ -57,10 +57,10 @@
 #define O_EPS 1e-4f
 #define O_PI 3.14159265358979323846 /* M_PI */
 
-typedef struct { float x, y, z; } V3;
+typedef struct { float x, y, z, w; } V3; /* Core.h Vec3: 16 B, constructors set w = 1 */
 typedef struct { float r, g, b; } Col;
 
-static V3 v3(float x, float y, float z) { V3 v; v.x = x; v.y = y; v.z = z; return v; }
+static V3 v3(float x, float y, float z) { V3 v; v.x = x; v.y = y; v.z = z; v.w = 1.0f; return v; }
 static V3 vadd(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 static V3 vsub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 static V3 vmuls(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
@@ -121,14 +121,21 @@ static void pcg_init(Pcg* p, uint64_t seed, uint64_t seq) {
 static float pcg_next(Pcg* p) { return (float)(pcg_u32(p) >> 8) * (1.0f / 16777216.0f); }
 
 /* ------------------------------------------------------------------ scene */
+/* Scene records in the reference's memory layout, so that the tile renderer's cache behaviour (and
+ * so the CPU baseline of bench.py) is the reference's: Vec3 is 16 B (Core.h), Vertex 40 B, Triangle
+ * 180 B in one std::vector (Geometry.h:62-71), BVHNode 56 B allocated one by one with `new`
+ * (64-B stride: 8-B allocator header), children in pairs l, r and then l's subtree before r's
+ * (BVHNode::buildRecursive, Geometry.h:387-390). The arithmetic does not depend on the layout. */
+typedef struct { V3 p; V3 n; float u, v; } Vtx;
 typedef struct {
-    V3 p[3], n[3];
-    float u[3], v[3];
+    Vtx vx[3];
     V3 e1, e2, nrm;
     float area, d;
     uint32_t mat;
 } Tri;
-typedef struct { V3 mn, mx; int l, r, start, end; } Node;
+typedef struct { V3 mn, mx; int r, r_hi, l, l_hi; int start, end; int heap[2]; } Node;
+_Static_assert(sizeof(Tri) == 180, "reference Triangle is 180 B");
+_Static_assert(sizeof(Node) == 64, "reference BVHNode allocation stride is 64 B");
 typedef struct { int w, h; const float* t; } Tex;
 
 struct or_scene {
@@ -183,9 +190,9 @@ static int tri_hit(const Tri* T, const Ray* r, float* t, float* u, float* v) {
     if (*t < 0) return 0;
     V3 p = vadd(r->o, vmuls(r->dir, *t));
     float inv_area = 1.0f / vdot(vcross(T->e1, T->e2), T->nrm);
-    *u = vdot(vcross(T->e1, vsub(p, T->p[1])), T->nrm) * inv_area;
+    *u = vdot(vcross(T->e1, vsub(p, T->vx[1].p)), T->nrm) * inv_area;
     if (*u < 0 || *u > 1.0f) return 0;
-    *v = vdot(vcross(T->e2, vsub(p, T->p[2])), T->nrm) * inv_area;
+    *v = vdot(vcross(T->e2, vsub(p, T->vx[2].p)), T->nrm) * inv_area;
     if (*v < 0 || (*u + *v) > 1.0f) return 0;
     return 1;
 }
@@ -334,10 +341,10 @@ static Shading shading_data(const struct or_scene* s, const Isect* is, const Ray
     if (!(is->t < FLT_MAX)) return sd;
     const Tri* T = &s->tri[is->id];
     sd.x = vadd(r->o, vmuls(r->dir, is->t));
-    V3 n = vadd(vadd(vmuls(T->n[0], is->alpha), vmuls(T->n[1], is->beta)), vmuls(T->n[2], is->gamma));
+    V3 n = vadd(vadd(vmuls(T->vx[0].n, is->alpha), vmuls(T->vx[1].n, is->beta)), vmuls(T->vx[2].n, is->gamma));
     sd.sN = vnorm(n);
-    sd.tu = (T->u[0] * is->alpha + T->u[1] * is->beta) + T->u[2] * is->gamma;
-    sd.tv = (T->v[0] * is->alpha + T->v[1] * is->beta) + T->v[2] * is->gamma;
+    sd.tu = (T->vx[0].u * is->alpha + T->vx[1].u * is->beta) + T->vx[2].u * is->gamma;
+    sd.tv = (T->vx[0].v * is->alpha + T->vx[1].v * is->beta) + T->vx[2].v * is->gamma;
     sd.bsdf = &s->mat[T->mat];
     if (sd.bsdf->two_sided && vdot(sd.wo, sd.sN) < 0) sd.sN = vneg(sd.sN);
     sd.frame = frame_from(sd.sN);
@@ -367,14 +374,14 @@ static Col compute_direct(const struct or_scene* s, const Shading* sd, Pcg* smp,
         float beta = r2 * sqrtf(r1);
         float gamma = 1.0f - (alpha + beta);
         float pdf = 1.0f / T->area;
-        V3 p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+        V3 p = vadd(vadd(vmuls(T->vx[0].p, alpha), vmuls(T->vx[1].p, beta)), vmuls(T->vx[2].p, gamma));
         ev_push(2, (float)li, p.x, p.y, p.z); /* area light sample point */
         const float* e = s->mat[T->mat].emission;
         Col emitted = col(e[0], e[1], e[2]);
         V3 wi = vsub(p, sd->x);
         float l = vlen2(wi);
         wi = vnorm(wi);
-        V3 gn = vmuls(T->nrm, vdot(T->n[0], T->nrm) > 0 ? 1.0f : -1.0f); /* Triangle::gNormal */
+        V3 gn = vmuls(T->nrm, vdot(T->vx[0].n, T->nrm) > 0 ? 1.0f : -1.0f); /* Triangle::gNormal */
         float G = (win_max(vdot(wi, sd->sN), 0.0f) * win_max(-vdot(wi, gn), 0.0f)) / l;
         if (G > 0) {
             if (scene_visible(s, sd->x, p, c))
@@ -466,14 +473,14 @@ static Col compute_direct_mis(const struct or_scene* s, const Shading* sd, Pcg* 
         float beta = r2 * sqrtf(r1);
         float gamma = 1.0f - (alpha + beta);
         pdf = 1.0f / T->area;
-        V3 p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+        V3 p = vadd(vadd(vmuls(T->vx[0].p, alpha), vmuls(T->vx[1].p, beta)), vmuls(T->vx[2].p, gamma));
         ev_push(2, (float)li, p.x, p.y, p.z); /* area light sample point */
         const float* e = s->mat[T->mat].emission;
         Col emitted = col(e[0], e[1], e[2]);
         V3 wi = vsub(p, sd->x);
         float l = vlen2(wi);
         wi = vnorm(wi);
-        V3 gn = vmuls(T->nrm, vdot(T->n[0], T->nrm) > 0 ? 1.0f : -1.0f);
+        V3 gn = vmuls(T->nrm, vdot(T->vx[0].n, T->nrm) > 0 ? 1.0f : -1.0f);
         float cos_surface = win_max(vdot(wi, sd->sN), 0.0f);
         float cos_light = win_max(-vdot(wi, gn), 0.0f);
         float G = cos_surface * cos_light / l;
@@ -650,29 +657,50 @@ or_scene* or_create(const rtg_scene_desc* d, int max_depth) {
         for (int k = 0; k < 3; ++k) {
             const float* p = d->positions + (size_t)i * 9 + k * 3;
             const float* n = d->normals + (size_t)i * 9 + k * 3;
-            T->p[k] = v3(p[0], p[1], p[2]);
-            T->n[k] = v3(n[0], n[1], n[2]);
-            T->u[k] = d->uvs[(size_t)i * 6 + k * 2];
-            T->v[k] = d->uvs[(size_t)i * 6 + k * 2 + 1];
+            T->vx[k].p = v3(p[0], p[1], p[2]);
+            T->vx[k].n = v3(n[0], n[1], n[2]);
+            T->vx[k].u = d->uvs[(size_t)i * 6 + k * 2];
+            T->vx[k].v = d->uvs[(size_t)i * 6 + k * 2 + 1];
         }
         T->mat = d->material[i];
-        T->e1 = vsub(T->p[2], T->p[1]);
-        T->e2 = vsub(T->p[0], T->p[2]);
+        T->e1 = vsub(T->vx[2].p, T->vx[1].p);
+        T->e2 = vsub(T->vx[0].p, T->vx[2].p);
         T->nrm = vnorm(vcross(T->e1, T->e2));
         T->area = vlen(vcross(T->e1, T->e2)) * 0.5f;
-        T->d = vdot(T->nrm, T->p[0]);
+        T->d = vdot(T->nrm, T->vx[0].p);
     }
+    /* node order of the reference's allocations: root, then for every internal node its (l, r) pair
+     * followed by l's subtree and r's subtree (an explicit stack of pending r subtrees) */
     s->node = (Node*)calloc((size_t)s->nnode, sizeof(Node));
+    int* pos = (int*)malloc((size_t)s->nnode * sizeof(int));
+    int* stk = (int*)malloc(((size_t)s->nnode + 1) * sizeof(int));
+    int next = 0, top = 0;
+    pos[0] = next++;
+    stk[top++] = 0;
+    while (top > 0) {
+        int i = stk[--top];
+        for (;;) {
+            const int32_t* L = d->node_links + (size_t)i * 4;
+            if (L[0] < 0 || L[1] < 0) break;
+            pos[L[0]] = next++;
+            pos[L[1]] = next++;
+            stk[top++] = L[1];
+            i = L[0];
+        }
+    }
     for (int i = 0; i < s->nnode; ++i) {
         const float* b = d->node_bounds + (size_t)i * 6;
         const int32_t* L = d->node_links + (size_t)i * 4;
-        s->node[i].mn = v3(b[0], b[1], b[2]);
-        s->node[i].mx = v3(b[3], b[4], b[5]);
-        s->node[i].l = L[0];
-        s->node[i].r = L[1];
-        s->node[i].start = L[2];
-        s->node[i].end = L[3];
+        Node* n = &s->node[pos[i]];
+        n->mn = v3(b[0], b[1], b[2]);
+        n->mx = v3(b[3], b[4], b[5]);
+        n->l = L[0] >= 0 ? pos[L[0]] : L[0];
+        n->r = L[1] >= 0 ? pos[L[1]] : L[1];
+        n->start = L[2];
+        n->end = L[3];
     }
+    free(pos);
+    free(stk);
     s->mat = (rtg_material*)calloc((size_t)d->n_materials + 1, sizeof(rtg_material));
     memcpy(s->mat, d->materials, d->n_materials * sizeof(rtg_material));
     size_t total = 0;
@@ -924,12 +952,12 @@ static void light_emit_sample(const struct or_scene* s, const Tri* T, Pcg* smp, 
     float beta = r2 * sqrtf(r1);
     float gamma = 1.0f - (alpha + beta);
     *pdf_pos = 1.0f / T->area;
-    *p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+    *p = vadd(vadd(vmuls(T->vx[0].p, alpha), vmuls(T->vx[1].p, beta)), vmuls(T->vx[2].p, gamma));
     float q2 = pcg_next(smp); /* cosineSampleHemisphere(sampler.next(), sampler.next()) */
     float q1 = pcg_next(smp);
     V3 wl = cosine_sample_hemisphere(q1, q2);
     *pdf_dir = (float)((wl.z >= 0.0f) ? (wl.z / O_PI) : 0.0f);
-    *gn = vmuls(T->nrm, vdot(T->n[0], T->nrm) > 0 ? 1.0f : -1.0f);
+    *gn = vmuls(T->nrm, vdot(T->vx[0].n, T->nrm) > 0 ? 1.0f : -1.0f);
     Frame fr = frame_from(*gn);
     *wi = to_world(&fr, wl);
     (void)s;
@@ -1122,9 +1150,9 @@ int or_light_emit(or_scene* s, int li, const float* draws, float* out) {
      * the sampling here with the draws in call order (r1, r2, then the direction's q2, q1) */
     float r1 = draws[0], r2 = draws[1], q2 = draws[2], q1 = draws[3];
     float alpha = 1 - sqrtf(r1), beta = r2 * sqrtf(r1), gamma = 1.0f - (alpha + beta);
-    V3 p = vadd(vadd(vmuls(T->p[0], alpha), vmuls(T->p[1], beta)), vmuls(T->p[2], gamma));
+    V3 p = vadd(vadd(vmuls(T->vx[0].p, alpha), vmuls(T->vx[1].p, beta)), vmuls(T->vx[2].p, gamma));
     V3 wl = cosine_sample_hemisphere(q1, q2);
-    V3 gn = vmuls(T->nrm, vdot(T->n[0], T->nrm) > 0 ? 1.0f : -1.0f);
+    V3 gn = vmuls(T->nrm, vdot(T->vx[0].n, T->nrm) > 0 ? 1.0f : -1.0f);
     Frame fr = frame_from(gn);
     V3 wi = to_world(&fr, wl);
     const float* e = s->mat[T->mat].emission;

@@ -471,3 +471,30 @@ def test_adaptive_render_many_frames_and_key_limit():
     after, spp_after = rt.film()
     assert spp_after == spp_before
     assert_bitexact(after, before, "film untouched by a rejected adaptive call")
+
+
+@pytest.mark.parametrize("case", ["cornell-mat", "bathroom", "coffee+GI", "synth20k"])
+def test_gpu_film_vs_reference_classes(case, synth20k):
+    """The GPU film against RayTracer::pathTrace restated on RTBase's own compiled classes
+    (oracle/_ref libref_rtm.so: the reference's BVH traversal, shading, BSDFs, lights, camera and
+    Film, with the shared transcendentals interposed), bit for bit: a film-level pin that does not
+    go through the C oracle."""
+    from oracle import pyref
+    if not pyref.available():
+        pytest.fail("oracle/_ref (libref_rtm.so) missing: build it where /root/reference exists")
+    if case == "synth20k":
+        import tempfile
+        d = tempfile.mkdtemp(prefix="rtg_s20k_")
+        write_synthetic_scene(d, n_tris=20000, seed=3, width=128, height=96)
+        path, kw, depth, spp, seed = d, dict(width=128, height=96), 4, 3, 42
+    else:
+        name, kw, depth, spp, seed = {
+            "cornell-mat": (os.path.join(SCENES, "cornell-mat"), dict(width=80, height=60), 8, 3, 99),
+            "bathroom": (staged("bathroom"), dict(width=96, height=54, skip_missing=True), 16, 2, 7),
+            "coffee+GI": (staged("coffee"), dict(width=80, height=100, skip_missing=True, envmap="GI.hdr"), 4, 3, 5),
+        }[case]
+        path = name
+    r = pyref.RefScene(path, kw["width"], kw["height"], kw.get("skip_missing", False), kw.get("envmap"), flavour="rtm")
+    ref, _ = r.render(spp, seed=seed, max_depth=depth, threads=8)
+    s = loadScene(path, **kw)
+    assert_bitexact(gpu_film(s, spp, seed=seed, max_depth=depth), ref, "GPU vs reference classes (%s)" % case)

@@ -137,3 +137,53 @@ def test_light_tracer_and_radiosity_oracles_are_deterministic():
     assert np.isfinite(a).all() and (a > 0).sum() > 100
     c = o.render_instant_radiosity(1, seed=3, n_vpl=10)
     assert np.isfinite(c).all() and (c > 0).sum() > 100
+
+
+# ---- film-level pin on the reference's own classes (oracle/_ref ref_render)
+REF_FILM_CASES = [
+    # (scene, kwargs, max_depth, spp, seed): glass / mirror / env (cornell-mat), C4's bathroom_f with
+    # JPEG/PNG textures at depth 16, C5's coffee_f + GI.hdr, and a synthetic env-lit scene
+    ("cornell-mat", dict(width=80, height=60), 8, 3, 99),
+    ("bathroom", dict(width=96, height=54, skip_missing=True), 16, 2, 7),
+    ("coffee", dict(width=80, height=100, skip_missing=True, envmap="GI.hdr"), 4, 3, 5),
+]
+
+
+def _ref_scene_dir(name):
+    from conftest import scene_path
+    p = scene_path(name)
+    if p is None:
+        pytest.skip("%s assets not available here" % name)
+    return p
+
+
+@pytest.mark.parametrize("flavour", ["libm", "rtm"])
+@pytest.mark.parametrize("case", range(len(REF_FILM_CASES)))
+def test_oracle_film_equals_reference_classes(case, flavour):
+    """The C oracle's integrator against RayTracer::pathTrace restated on RTBase's own compiled
+    classes (ref_render: Scene::traverse/visible, calculateShadingData, BSDF::sample/evaluate,
+    Light::sample, Camera, Film::splat from /root/reference), with glibc and with the shared
+    transcendentals: films identical bit for bit, and the same closest-hit / shadow ray counts."""
+    from oracle import pyref
+    if not pyref.available():
+        pytest.skip("oracle/_ref not built")
+    name, kw, depth, spp, seed = REF_FILM_CASES[case]
+    path = _ref_scene_dir(name)
+    r = pyref.RefScene(path, kw["width"], kw["height"], kw.get("skip_missing", False), kw.get("envmap"), flavour=flavour)
+    ref, rc = r.render(spp, seed=seed, max_depth=depth, threads=8)
+    s = loadScene(path, **kw)
+    mine, oc = Oracle(s, depth, flavour).render(spp, seed=seed, threads=8, count=True)
+    assert np.array_equal(mine.view(np.uint32), ref.view(np.uint32)), (mine != ref).sum()
+    assert rc.tolist() == oc[:3].tolist()
+
+
+def test_c1_known_answer_from_reference_classes():
+    """SURVEY.md §8c's C1 md5 (the reference integrator built in the survey, glibc) is reproduced by
+    ref_render on the reference's own classes, so both the oracle and ref_render are pinned to it."""
+    from oracle import pyref
+    if not pyref.available():
+        pytest.skip("oracle/_ref not built")
+    r = pyref.RefScene(os.path.join(SCENES, "cornell-box"), 256, 256, False)
+    film, c = r.render(4, seed=1234, max_depth=4, threads=8)
+    assert hashlib.md5((film / np.float32(4)).astype(np.float32).tobytes()).hexdigest() == "2fe4126eaf3a9c654e6beea0a1da9ba9"
+    assert c.tolist() == [262144, 702961, 429793]
