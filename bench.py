@@ -24,7 +24,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, same guide (§L2)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
+ROOF_TABLE_MIB = 69  # the hot scene of C3: 21 MB wide nodes + 48 MB triangle records
+# per-ray queue id + ray origin + direction reads and the hit / visibility write (16-B requests)
+REQ_PER_RAY_IO = 4.0
+
+
+def request_ceiling():
+    """Best request rate of the ceiling microbenchmark on the table matching k_trace's hot scene."""
+    try:
+        rows = [json.loads(l) for l in open(ROOF_SWEEP) if l.strip().startswith("{")]
+    except OSError:
+        return None
+    rows = [r for r in rows if r.get("table_mib") == ROOF_TABLE_MIB]
+    return max(rows, key=lambda r: r["g_req_per_s"]) if rows else None
 # BASELINE.json configs (SURVEY.md §8): scene, size, spp, MAX_DEPTH. C1 is the CPU-only case.
 CONFIGS = {
     "C2": {"scene": "cornell-box", "width": 1024, "height": 1024, "spp": 64, "depth": 8},
@@ -210,9 +225,19 @@ def main():
     ms_step = t_max * 1e3 / a.steps
 
     # roofline for the dominant kernel, k_trace (one launch per bounce traces the extension rays of
-    # bounce b and the shadow rays of bounce b-1): algorithmic bytes per ray
-    # B = 32 B x box tests + 36 B x triangle tests + 48 B ray I/O, with the box and
-    # triangle tests of the reference's own walk (BVH2, counted on the same workload)
+    # bounce b and the shadow rays of bounce b-1). Its limiter is the vector-memory request rate
+    # (TA busy ~87 %): every lane of a node step issues four 16-B loads of its own 64-B record at a
+    # data-dependent address (triangles: three). achieved = the walk's 16-B requests (counted on the
+    # same workload by the untimed counting pass) / the k_trace HIP-event time of the timed region;
+    # peak = the same request shape's ceiling measured by tools/micro/roof.hip (dependent random 64-B
+    # per-lane records from a 69 MiB table, the hot scene's size, at k_trace's occupancy).
+    n_steps = a.steps
+    req_step = (4.0 * cw["node_lane_steps"] + 3.0 * (cw["tri_tests"] + cw["shadow_tri_tests"])
+                + REQ_PER_RAY_IO * (cw["extension_rays"] + cw["shadow_rays"]))
+    req_totals = np.array([req_step * n_steps], dtype=np.float64)
+    # SURVEY.md §8d algorithmic bytes B = 32 B x box tests + 36 B x triangle tests + 48 B ray I/O,
+    # with the box / triangle tests of the reference's own walk (BVH2, counted on the same workload);
+    # these bytes are served by L1/L2/Infinity Cache, so they are compared with the L2 bandwidth
     boxes_per_ray = c_nodes / max(c_ext, 1)
     tris_per_ray = c_tris / max(c_ext, 1)
     b_ray = 32.0 * boxes_per_ray + 36.0 * tris_per_ray + 48.0
@@ -220,9 +245,17 @@ def main():
     s_tris_per_ray = s_tris / max(c_sh, 1)
     b_sray = 32.0 * s_boxes_per_ray + 36.0 * s_tris_per_ray + 48.0
     # time and rays both summed over ranks and launches
-    achieved_gbs = (b_ray * ext_rays + b_sray * shadow_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
-    # the PMC summary is per launch of the default workload (C3, 64 spp, one rank): other workloads
-    # (configs, shards, N > 1 ranks) have other launch sizes and report no measured traffic
+    algo_gbs = (b_ray * ext_rays + b_sray * shadow_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
+    if world > 1:
+        import torch
+        rt_ = torch.tensor(req_totals, dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(rt_, op=dist.ReduceOp.SUM)
+        req_totals = rt_.cpu().numpy()
+    achieved_req = req_totals[0] / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
+    ceiling = request_ceiling()
+    avg_launch_s = extend_ms / max(extend_launches, 1) / 1e3
+    # measured HBM traffic per launch (PMC, profiles/): only for the profiled workload (C3, 64 spp,
+    # one rank); other configs, shards and N > 1 have other launch sizes and report null
     traffic = None
     profiled = (a.config == "C3" and world == 1 and a.shard_of <= 1 and a.spp == 64 and a.tris == 1_000_000
                 and (a.width, a.height) == (1024, 1024) and a.max_depth == 4)
@@ -261,35 +294,49 @@ def main():
                            a.width, a.height, a.spp, a.max_depth),
                        "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
                        "max_depth": a.max_depth, "parallelism": "tile-sharded x%d + RCCL film reduce" % world},
-            "roofline": {"bound": "hbm", "kernel": "k_trace (extension + shadow rays)",
-                         "achieved": None if achieved_gbs is None else round(achieved_gbs, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": None if achieved_gbs is None else round(achieved_gbs / HBM_PEAK_GBS, 4),
+            "roofline": {"bound": "vmem-requests", "kernel": "k_trace (extension + shadow rays)",
+                         "achieved": None if achieved_req is None else round(achieved_req, 1),
+                         "peak": None if ceiling is None else round(ceiling["g_req_per_s"], 1),
+                         "unit": "G 16-B vector-memory requests/s",
+                         "frac": (round(achieved_req / ceiling["g_req_per_s"], 4)
+                                  if achieved_req and ceiling else None),
                          "traffic": traffic,
-                         # L2->fabric bytes per launch (PMC, profiles/) over this run's average launch
-                         "traffic_gbs": (round(traffic / (extend_ms / max(extend_launches, 1) / 1e3) / 1e9, 1)
-                                         if traffic and extend_ms > 0 else None),
-                         "traffic_frac": (round(traffic / (extend_ms / max(extend_launches, 1) / 1e3) / 1e9
-                                                / HBM_PEAK_GBS, 4) if traffic and extend_ms > 0 else None),
-                         "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
-                         "tri_tests_per_ray": round(tris_per_ray, 2),
-                         "bytes_per_shadow_ray": round(b_sray, 1),
-                         "shadow_box_tests_per_ray": round(s_boxes_per_ray, 2),
-                         "shadow_tri_tests_per_ray": round(s_tris_per_ray, 2),
-                         "limiter": "vector-memory address/L1 request rate (TA busy ~87 %); the scene is "
-                                    "served from L2/Infinity Cache, so algorithmic bytes can exceed the HBM "
-                                    "peak (DESIGN.md §4)",
+                         "ceiling": (None if ceiling is None else
+                                     "tools/micro/roof.hip, %s: dependent random 64-B per-lane records (4 x "
+                                     "dwordx4), %d MiB table, %d VALU/step, k_trace's occupancy"
+                                     % (os.path.relpath(ROOF_SWEEP, ROOT), ceiling["table_mib"],
+                                        ceiling["valu_per_step"])),
+                         "requests_per_ray": round(req_step / max(cw["extension_rays"] + cw["shadow_rays"], 1), 2),
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                         "hbm": {"bytes_per_launch": traffic,
+                                 "achieved_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic and extend_ms > 0 else None,
+                                 "peak_gbs": HBM_PEAK_GBS,
+                                 "frac": (round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4)
+                                          if traffic and extend_ms > 0 else None),
+                                 "source": "rocprofv3 FETCH_SIZE (x1: calibrated for 64-B gathers, "
+                                           "profiles/r02_fetch_calibration.json) + WRITE_SIZE, per launch"},
+                         "algorithmic": {"definition": "SURVEY.md 8d: 32 B x box tests + 36 B x triangle tests + "
+                                                       "48 B per ray, reference BVH2 walk counts",
+                                         "achieved_gbs": None if algo_gbs is None else round(algo_gbs, 1),
+                                         "served_by": "L1 / L2 / Infinity Cache (scene ~70 MB hot)",
+                                         "l2_peak_gbs": L2_PEAK_GBS,
+                                         "l2_frac": None if algo_gbs is None else round(algo_gbs / L2_PEAK_GBS, 4),
+                                         "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
+                                         "tri_tests_per_ray": round(tris_per_ray, 2),
+                                         "bytes_per_shadow_ray": round(b_sray, 1),
+                                         "shadow_box_tests_per_ray": round(s_boxes_per_ray, 2),
+                                         "shadow_tri_tests_per_ray": round(s_tris_per_ray, 2)},
                          "walk": "bvh2" if a.bvh2 else ("bvh4 (collapsed from the reference BVH2)" if os.environ.get("RTG_REBUILD") == "0" else "bvh4 (collapsed from an own 3-axis SAH tree over the reference leaves)"),
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
+                         "node_steps_per_ray": round(cw["node_lane_steps"] / max(cw["extension_rays"] + cw["shadow_rays"], 1), 2),
                          "pops_per_ray": round(cw["pops"] / max(cw["extension_rays"], 1), 2),
                          "cullable_pops_per_ray": round(cw["cullable_pops"] / max(cw["extension_rays"], 1), 2),
                          # node: lanes stepping a node per loop iteration; leaf: lanes running a
                          # parked leaf per leaf phase; leaf phases per iteration
                          "lane_util_node_leaf": [round(cw["node_lane_steps"] / max(cw["lane_slots"], 1), 3),
                                                  round(cw["leaf_lane_steps"] / max(cw["leaf_phase_slots"], 1), 3),
-                                                 round(cw["leaf_phase_slots"] / max(cw["lane_slots"], 1), 3)],
-                         "avg_launch_ms": round(extend_ms / max(extend_launches, 1), 4)},
+                                                 round(cw["leaf_phase_slots"] / max(cw["lane_slots"], 1), 3)]},
             "kernel_ms_per_step_rank0": {"trace": round(local_kernel_ms[0] / a.steps, 2),
                                          "generate_shade_accumulate": round(local_kernel_ms[2] / a.steps, 2)},
             "cpu_baseline": cpu,

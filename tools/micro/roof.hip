@@ -1,0 +1,106 @@
+// roof.hip — the request-rate ceiling that bounds k_trace, and the FETCH_SIZE
+// calibration for its access shape.
+//
+// k_trace is bound by vector-memory requests, not bytes: every lane of a node step issues four
+// 16-B loads (global_load_dwordx4) of its own 64-B record at a data-dependent address, and the
+// next record's address depends on this one. This kernel does exactly that and nothing else: per
+// lane a dependent random chain of 64-B records (4 x dwordx4 each) over a table of T MiB, with V
+// dependent VALU ops per step, at k_trace's occupancy (256-thread blocks, 6 waves per SIMD, 1536
+// blocks on 256 CUs). It reports G 16-B requests/s = lanes x steps x 4 / time.
+//
+//   roof                      sweep: tables 21 / 69 / 1024 MiB x VALU 0 / 32 / 64 -> JSON lines
+//   roof T V STEPS            one configuration (for rocprofv3 --pmc passes: FETCH_SIZE
+//                             calibration on a table larger than the 256 MiB Infinity Cache)
+// Build: hipcc --offload-arch=gfx950 -O3 -o roof roof.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+__device__ inline unsigned hash(unsigned x) {
+    x ^= x >> 16; x *= 0x7feb352d; x ^= x >> 15; x *= 0x846ca68b; x ^= x >> 16;
+    return x;
+}
+
+template <int VALU>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6)))
+void k_chain(const float4* __restrict__ tab, unsigned nrec, int steps, float* out) {
+    const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned idx = hash(gid * 2654435761u + 12345u) % nrec;
+    float acc = 0.f;
+    for (int s = 0; s < steps; ++s) {
+        const float4* r = tab + (size_t)idx * 4;
+        const float4 a = r[0], b = r[1], c = r[2], d = r[3];
+        float sum = (((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w))) +
+                    (((c.x + c.y) + (c.z + c.w)) + ((d.x + d.y) + (d.z + d.w)));
+#pragma unroll
+        for (int v = 0; v < VALU; ++v) sum = __builtin_fmaf(sum, 1.0000001f, a.y * (float)v);
+        acc += sum;
+        idx = hash(idx ^ __float_as_uint(sum)) % nrec;
+    }
+    out[gid] = acc;
+}
+
+static double run(int valu, const float4* d, unsigned nrec, float* out, int blocks, int steps, int reps) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    float best = 1e30f;
+    for (int rep = 0; rep < reps; ++rep) {
+        (void)hipEventRecord(a);
+        switch (valu) {
+            case 0: hipLaunchKernelGGL(k_chain<0>, dim3(blocks), dim3(256), 0, 0, d, nrec, steps, out); break;
+            case 32: hipLaunchKernelGGL(k_chain<32>, dim3(blocks), dim3(256), 0, 0, d, nrec, steps, out); break;
+            default: hipLaunchKernelGGL(k_chain<64>, dim3(blocks), dim3(256), 0, 0, d, nrec, steps, out); break;
+        }
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, a, b);
+        if (ms < best) best = ms;
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return best;
+}
+
+int main(int argc, char** argv) {
+    int dev_cus = 0;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, 0);
+    const int blocks = (dev_cus > 0 ? dev_cus : 256) * 6;  // 6 waves per SIMD, 4 SIMDs, 4 waves per block
+    const size_t maxmib = 1024;
+    const size_t nfl = maxmib * 1048576 / 4;
+    float4* d = nullptr;
+    float* out = nullptr;
+    if (hipMalloc(&d, nfl * 4) != hipSuccess || hipMalloc(&out, (size_t)blocks * 256 * 4) != hipSuccess) {
+        std::fprintf(stderr, "hipMalloc failed\n");
+        return 1;
+    }
+    {
+        std::vector<float> h(nfl);
+        for (size_t i = 0; i < nfl; ++i) h[i] = (float)(i % 97) * 0.01f;
+        (void)hipMemcpy(d, h.data(), nfl * 4, hipMemcpyHostToDevice);
+    }
+    auto one = [&](size_t mib, int valu, int steps, int reps) {
+        const unsigned nrec = (unsigned)(mib * 1048576 / 64);
+        const double ms = run(valu, d, nrec, out, blocks, steps, reps);
+        const double lanes = (double)blocks * 256;
+        const double req = lanes * steps * 4;
+        std::printf("{\"table_mib\": %zu, \"valu_per_step\": %d, \"blocks\": %d, \"steps\": %d, \"ms\": %.4f, "
+                    "\"g_req_per_s\": %.2f, \"g_lane_steps_per_s\": %.2f, \"record_bytes\": %.0f, "
+                    "\"requested_gbs\": %.1f}\n",
+                    mib, valu, blocks, steps, ms, req / ms / 1e6, lanes * steps / ms / 1e6, lanes * steps * 64.0,
+                    lanes * steps * 64.0 / ms / 1e6);
+        std::fflush(stdout);
+    };
+    if (argc >= 4) {
+        one((size_t)std::atoi(argv[1]), std::atoi(argv[2]), std::atoi(argv[3]), 1);
+    } else {
+        for (size_t mib : {21, 69, 1024})
+            for (int valu : {0, 32, 64}) one(mib, valu, 256, 3);
+    }
+    (void)hipFree(d);
+    (void)hipFree(out);
+    return 0;
+}

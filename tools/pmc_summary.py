@@ -1,7 +1,11 @@
 """Summarise rocprofv3 runs into profiles/: kernel-trace stats + FETCH_SIZE / WRITE_SIZE per launch.
 
-gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts half the bytes of a wide
-coalesced stream; we report raw and x2-corrected read bytes. WRITE_SIZE (KiB) is taken as-is.
+gfx950 corrections: FETCH_SIZE (KiB) counts 64 B per L2->fabric read request. For a wide coalesced
+stream that is half the bytes (MI355X_MICROARCH.md §HBM: x2). For k_trace's 64-B per-lane record
+gathers it is exactly the requested bytes of the L2-missing records (profiles/r02_fetch_calibration.json,
+tools/micro/roof.hip on a 1 GiB table): x1. So k_trace's reads are taken x1 (its per-ray queue/ray
+stream reads, ~10 % of its fetches, are then under-counted by half) and every other kernel's x2.
+WRITE_SIZE (KiB) is taken as-is.
 """
 import csv, json, sys, collections
 
@@ -19,13 +23,14 @@ def main(fetch_csv, write_csv, stats_csv, out_json, dram_csv=None):
     rd = per_kernel(dram_csv, "TCC_EA0_RDREQ_DRAM_sum") if dram_csv else {}
     stats = {r["Name"]: r for r in csv.DictReader(open(stats_csv))}
     out = {"note": "per-launch averages; FETCH_SIZE/WRITE_SIZE in KiB from rocprofv3 --pmc (separate passes); "
-                   "read bytes corrected x2 for gfx950 wide-stream under-count", "kernels": {}}
+                   "read bytes: k_trace x1 (64-B gathers, profiles/r02_fetch_calibration.json), other kernels x2 "
+                   "(gfx950 wide-stream under-count)", "kernels": {}}
     for k in sorted(set(f) | set(w)):
         fk = sum(f.get(k, [0])) / max(len(f.get(k, [])), 1)
         wk = sum(w.get(k, [0])) / max(len(w.get(k, [])), 1)
         st = stats.get(k, {})
         out["kernels"][k] = {"launches_pmc": len(f.get(k, [])), "fetch_kib_raw": round(fk, 1),
-                             "read_bytes_corrected": round(fk * 1024 * 2), "write_bytes": round(wk * 1024),
+                             "read_bytes_corrected": round(fk * 1024 * (1 if "k_trace" in k else 2)), "write_bytes": round(wk * 1024),
                              "avg_ns_trace": float(st["AverageNs"]) if st else None,
                              "calls_trace": int(st["Calls"]) if st else None}
         if k in rq and sum(rq[k]) > 0:

@@ -12,7 +12,7 @@ for blk in md.split('  - .agpr_count')[1:]:
     name = re.search(r'\.name:\s+(\S+)', blk).group(1)
     if name.startswith(('_Z7k_traceILb0E', '_Z7k_shadeILb0E')):
         g = lambda k: re.search(r'\.' + k + r':\s+(\d+)', blk).group(1)
-        out.append('%s v%s/spill%s s-spill%s' % (name[7:14], g('vgpr_count'), g('vgpr_spill_count'), g('sgpr_spill_count')))
+        out.append('%s v%s/spill%s s-spill%s' % (name[7:20], g('vgpr_count'), g('vgpr_spill_count'), g('sgpr_spill_count')))
 print(repr(sys.argv[1]), ' | '.join(out))
 PY
 done
