@@ -199,6 +199,28 @@ int  rtg_render_instant_radiosity(rtg_handle* h, uint32_t first_frame, uint32_t 
 int  rtg_render_adaptive(rtg_handle* h, uint32_t first_sample, uint64_t seed, uint32_t init_samples,
                          uint32_t max_samples, uint32_t min_samples, uint32_t* tile_samples);
 
+/* ---- one node, several GPUs (rtg_multi.hip). RayTracer::pathTracerTileBased spreads 32x32 tiles
+ * over numProcs CPU threads (Renderer.h:836-853, numProcs from :52-54); here the tiles are spread
+ * over devices: rank r of N renders every sample of the tiles with (tile_x + tile_y) % N == r
+ * (rtg_tiles_for_rank; the partition of raytracingrenderer_amd/distributed.py), one host thread and
+ * one handle per device, and rtg_group_reduce sums the float films into devices[0] with one RCCL
+ * ncclReduce (ncclCommInitAll, single process). The reduced film is bit-identical to a one-device
+ * render. A device list with repeats (N ranks rehearsed on fewer GPUs) sums through host memory. */
+typedef struct rtg_group rtg_group;
+int  rtg_tiles_for_rank(uint32_t width, uint32_t height, int rank, int world, uint32_t* tile_ids /* or NULL */,
+                        uint32_t* n_tiles);
+int  rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* desc, rtg_group** out);
+void rtg_group_destroy(rtg_group* g);
+int  rtg_group_size(rtg_group* g);
+rtg_handle* rtg_group_handle(rtg_group* g, int rank);  /* e.g. for rtg_get_stats; owned by the group */
+int  rtg_group_set_options(rtg_group* g, int max_depth, int flags, uint32_t max_paths);
+int  rtg_group_render(rtg_group* g, uint32_t first_sample, uint32_t n_samples, uint64_t seed);
+int  rtg_group_reduce(rtg_group* g);  /* the films stay per device; the sum goes to a separate buffer */
+int  rtg_group_film_read(rtg_group* g, float* rgb_sum /* width*height*3 */, uint32_t* spp);  /* reduces if needed */
+int  rtg_group_clear(rtg_group* g);
+double rtg_group_reduce_ms(rtg_group* g);  /* device time of the last reduce */
+int  rtg_group_uses_rccl(rtg_group* g);    /* 1: RCCL communicator, 0: host-memory sum (repeated devices) */
+
 /* Film access: the unnormalised sum (Film::film) and the sample count (Film::SPP). */
 int  rtg_film_read(rtg_handle* h, float* rgb_sum /* width*height*3 */, uint32_t* spp);
 int  rtg_film_copy_device(rtg_handle* h, void* dst_device /* width*height*3 floats */);

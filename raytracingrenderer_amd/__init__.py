@@ -3,8 +3,8 @@
 The hot path (RayTracer::render) runs as HIP kernels in lib/librtg.so behind include/rtg.h;
 scene loading / BVH build / HDR output run in lib/librth.so behind include/rth.h.
 """
-from .renderer import (NativeError, RayTracer, Scene, loadScene, read_hdr, save_hdr, save_png,  # noqa: F401
-                       tonemap, write_synthetic_scene)
+from .renderer import (NativeError, RayTracer, RayTracerGroup, Scene, loadScene, read_hdr,  # noqa: F401
+                       save_hdr, save_png, tonemap, write_synthetic_scene)
 
-__all__ = ["RayTracer", "Scene", "loadScene", "save_hdr", "save_png", "tonemap", "read_hdr",
+__all__ = ["RayTracer", "RayTracerGroup", "Scene", "loadScene", "save_hdr", "save_png", "tonemap", "read_hdr",
            "write_synthetic_scene", "NativeError"]

@@ -92,6 +92,19 @@ RTG_EXPORTS = [
     ("rtg_trace_closest", C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
     ("rtg_trace_visible", C.c_int, [C.c_void_p, f32p, C.c_uint32, i32p]),
     ("rtg_probe_bsdf", C.c_int, [f32p, C.c_uint32, f32p]),
+    # one node, several GPUs (rtg_multi.hip): tile stripes per device + one RCCL film reduce
+    ("rtg_tiles_for_rank", C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.c_int, u32p, u32p]),
+    ("rtg_group_create", C.c_int, [i32p, C.c_int, C.POINTER(rtg_scene_desc), C.POINTER(C.c_void_p)]),
+    ("rtg_group_destroy", None, [C.c_void_p]),
+    ("rtg_group_size", C.c_int, [C.c_void_p]),
+    ("rtg_group_handle", C.c_void_p, [C.c_void_p, C.c_int]),
+    ("rtg_group_set_options", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_uint32]),
+    ("rtg_group_render", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64]),
+    ("rtg_group_reduce", C.c_int, [C.c_void_p]),
+    ("rtg_group_film_read", C.c_int, [C.c_void_p, f32p, u32p]),
+    ("rtg_group_clear", C.c_int, [C.c_void_p]),
+    ("rtg_group_reduce_ms", C.c_double, [C.c_void_p]),
+    ("rtg_group_uses_rccl", C.c_int, [C.c_void_p]),
 ]
 
 RTH_EXPORTS = [

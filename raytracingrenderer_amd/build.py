@@ -23,7 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RTG_ARCH", "gfx950")
 
 HOST_SRC = ["host/image_io.cpp", "host/jpeg_decode.cpp", "host/gem_json.cpp", "host/scene_front.cpp"]
-DEVICE_SRC = ["device/rtg_kernels.hip", "device/rtg_light.hip"]
+DEVICE_SRC = ["device/rtg_kernels.hip", "device/rtg_light.hip", "device/rtg_multi.hip"]
 
 
 def _newer(out, deps):
@@ -65,7 +65,7 @@ def build_device(force=False):
     src = [os.path.join(CSRC, s) for s in DEVICE_SRC]
     if force or _newer(out, _deps(src)):
         _run([HIPCC, "--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-std=c++17",
-              "-fPIC", "-shared", "-o", out] + src)
+              "-fPIC", "-shared", "-o", out] + src + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
     return out
 
 

@@ -1,0 +1,232 @@
+// rtg_multi.hip — one-node multi-GPU rendering behind the C-ABI (include/rtg.h, rtg_group_*).
+//
+// RTBase's only parallelism is the tile pool of RayTracer::pathTracerTileBased (Renderer.h:836-853:
+// numProcs threads pop 32x32 tiles from a shared queue, Renderer.h:52-54). Here the tiles are
+// spread over the GPUs of one node instead: device r renders every sample of the tiles with
+// (tile_x + tile_y) % N == r (diagonal stripes, the same partition as raytracingrenderer_amd/
+// distributed.py), one host thread and one rtg_handle per device, and the float films are summed
+// into the first device with one RCCL reduce over xGMI (ncclCommInitAll over the devices, single
+// process). Tile supports are disjoint and every other device adds +0.0, so the reduced film is
+// bit-identical to a one-GPU render, whatever the reduction order.
+//
+// A device list that repeats a device (rehearsing N ranks on one GPU) cannot form an RCCL
+// communicator; the films are then summed through host memory in rank order (same bits).
+#include "rtg_internal.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+struct rtg_group {
+    std::vector<int> devices;
+    std::vector<rtg_handle*> h;
+    std::vector<std::vector<uint32_t>> tiles;  // per rank
+    std::vector<ncclComm_t> comms;             // empty: host reduce (repeated devices)
+    float* d_sum = nullptr;                    // reduced film on devices[0]
+    uint32_t W = 0, H = 0;
+    uint32_t reduced_spp = 0;
+    bool reduced = false;
+    double reduce_ms = 0.0;
+};
+
+extern "C" {
+
+int rtg_tiles_for_rank(uint32_t width, uint32_t height, int rank, int world, uint32_t* tile_ids, uint32_t* n_tiles) {
+    if (!n_tiles || world < 1 || rank < 0 || rank >= world) {
+        g_err = "rtg_tiles_for_rank: bad argument";
+        return RTG_ERR_ARG;
+    }
+    const uint32_t tx = (width + 31) / 32, ty = (height + 31) / 32;
+    uint32_t n = 0;
+    for (uint32_t t = 0; t < tx * ty; ++t)
+        if (((t % tx) + (t / tx)) % (uint32_t)world == (uint32_t)rank) {
+            if (tile_ids) tile_ids[n] = t;
+            ++n;
+        }
+    *n_tiles = n;
+    return RTG_OK;
+}
+
+void rtg_group_destroy(rtg_group* g) {
+    if (!g) return;
+    for (ncclComm_t c : g->comms) (void)ncclCommDestroy(c);
+    if (g->d_sum) {
+        (void)hipSetDevice(g->devices[0]);
+        (void)hipFree(g->d_sum);
+    }
+    for (rtg_handle* h : g->h) rtg_destroy(h);
+    delete g;
+}
+
+int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* desc, rtg_group** out) {
+    if (!devices || n_devices < 1 || !desc || !out) {
+        g_err = "rtg_group_create: bad argument";
+        return RTG_ERR_ARG;
+    }
+    *out = nullptr;
+    rtg_group* g = new rtg_group();
+    g->devices.assign(devices, devices + n_devices);
+    g->W = desc->camera.width;
+    g->H = desc->camera.height;
+    for (int r = 0; r < n_devices; ++r) {
+        rtg_handle* h = nullptr;
+        const int rc = rtg_create(devices[r], desc, &h);
+        if (rc) {
+            rtg_group_destroy(g);
+            return rc;
+        }
+        g->h.push_back(h);
+        uint32_t n = 0;
+        rtg_tiles_for_rank(g->W, g->H, r, n_devices, nullptr, &n);
+        g->tiles.emplace_back(n);
+        rtg_tiles_for_rank(g->W, g->H, r, n_devices, g->tiles.back().data(), &n);
+    }
+    std::vector<int> sorted(g->devices);
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (distinct) {
+        g->comms.resize(n_devices);
+        const ncclResult_t nr = ncclCommInitAll(g->comms.data(), n_devices, g->devices.data());
+        if (nr != ncclSuccess) {
+            g->comms.clear();
+            g_err = std::string("ncclCommInitAll: ") + ncclGetErrorString(nr);
+            rtg_group_destroy(g);
+            return RTG_ERR_HIP;
+        }
+    }
+    if (hipSetDevice(g->devices[0]) != hipSuccess ||
+        hipMalloc((void**)&g->d_sum, (size_t)g->W * g->H * 3 * sizeof(float)) != hipSuccess) {
+        g_err = "rtg_group_create: film allocation failed";
+        rtg_group_destroy(g);
+        return RTG_ERR_HIP;
+    }
+    *out = g;
+    return RTG_OK;
+}
+
+int rtg_group_size(rtg_group* g) { return g ? (int)g->h.size() : 0; }
+
+rtg_handle* rtg_group_handle(rtg_group* g, int rank) {
+    return (g && rank >= 0 && rank < (int)g->h.size()) ? g->h[rank] : nullptr;
+}
+
+int rtg_group_set_options(rtg_group* g, int max_depth, int flags, uint32_t max_paths) {
+    if (!g) return RTG_ERR_ARG;
+    for (rtg_handle* h : g->h) {
+        const int rc = rtg_set_options(h, max_depth, flags, max_paths);
+        if (rc) return rc;
+    }
+    return RTG_OK;
+}
+
+int rtg_group_render(rtg_group* g, uint32_t first_sample, uint32_t n_samples, uint64_t seed) {
+    if (!g) return RTG_ERR_ARG;
+    const size_t n = g->h.size();
+    std::vector<int> rc(n, RTG_OK);
+    std::vector<std::string> err(n);
+    auto run = [&](size_t r) {
+        const std::vector<uint32_t>& t = g->tiles[r];
+        if (t.empty()) return;  // more devices than tiles: this rank's film stays zero
+        rc[r] = rtg_render(g->h[r], first_sample, n_samples, seed, t.data(), (uint32_t)t.size());
+        if (rc[r]) err[r] = rtg_last_error();  // g_err is thread-local
+    };
+    if (n == 1) {
+        run(0);
+    } else {
+        std::vector<std::thread> pool;
+        for (size_t r = 0; r < n; ++r) pool.emplace_back(run, r);
+        for (auto& t : pool) t.join();
+    }
+    g->reduced = false;
+    for (size_t r = 0; r < n; ++r)
+        if (rc[r]) {
+            g_err = "rank " + std::to_string(r) + ": " + err[r];
+            return rc[r];
+        }
+    return RTG_OK;
+}
+
+int rtg_group_reduce(rtg_group* g) {
+    if (!g) return RTG_ERR_ARG;
+    const size_t n = g->h.size();
+    const size_t count = (size_t)g->W * g->H * 3;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPOK(hipSetDevice(g->devices[0]));
+    HIPOK(hipEventCreate(&e0));
+    HIPOK(hipEventCreate(&e1));
+    HIPOK(hipEventRecord(e0, g->h[0]->stream));
+    if (!g->comms.empty()) {
+        // every rank's film (summed in sample order on its device) -> device 0, ncclSum
+        if (ncclGroupStart() != ncclSuccess) { g_err = "ncclGroupStart failed"; return RTG_ERR_HIP; }
+        for (size_t r = 0; r < n; ++r) {
+            HIPOK(hipSetDevice(g->devices[r]));
+            const ncclResult_t nr = ncclReduce(g->h[r]->d_film, r == 0 ? g->d_sum : nullptr, count, ncclFloat, ncclSum, 0,
+                                               g->comms[r], g->h[r]->stream);
+            if (nr != ncclSuccess) {
+                (void)ncclGroupEnd();
+                g_err = std::string("ncclReduce: ") + ncclGetErrorString(nr);
+                return RTG_ERR_HIP;
+            }
+        }
+        const ncclResult_t nr = ncclGroupEnd();
+        if (nr != ncclSuccess) { g_err = std::string("ncclGroupEnd: ") + ncclGetErrorString(nr); return RTG_ERR_HIP; }
+        for (size_t r = 0; r < n; ++r) {
+            HIPOK(hipSetDevice(g->devices[r]));
+            HIPOK(hipStreamSynchronize(g->h[r]->stream));
+        }
+    } else {
+        // repeated devices: rank order through host memory
+        std::vector<float> sum(count, 0.0f), f(count);
+        for (size_t r = 0; r < n; ++r) {
+            uint32_t spp = 0;
+            const int rc = rtg_film_read(g->h[r], f.data(), &spp);
+            if (rc) return rc;
+            for (size_t i = 0; i < count; ++i) sum[i] = sum[i] + f[i];
+        }
+        HIPOK(hipSetDevice(g->devices[0]));
+        HIPOK(hipMemcpy(g->d_sum, sum.data(), count * sizeof(float), hipMemcpyHostToDevice));
+    }
+    HIPOK(hipSetDevice(g->devices[0]));
+    HIPOK(hipEventRecord(e1, g->h[0]->stream));
+    HIPOK(hipEventSynchronize(e1));
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    g->reduce_ms = ms;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    g->reduced_spp = g->h[0]->spp;
+    g->reduced = true;
+    return RTG_OK;
+}
+
+int rtg_group_film_read(rtg_group* g, float* rgb_sum, uint32_t* spp) {
+    if (!g) return RTG_ERR_ARG;
+    if (!g->reduced) {
+        const int rc = rtg_group_reduce(g);
+        if (rc) return rc;
+    }
+    HIPOK(hipSetDevice(g->devices[0]));
+    if (rgb_sum) HIPOK(hipMemcpy(rgb_sum, g->d_sum, (size_t)g->W * g->H * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    if (spp) *spp = g->reduced_spp;
+    return RTG_OK;
+}
+
+int rtg_group_clear(rtg_group* g) {
+    if (!g) return RTG_ERR_ARG;
+    for (rtg_handle* h : g->h) {
+        const int rc = rtg_clear(h);
+        if (rc) return rc;
+    }
+    g->reduced = false;
+    return RTG_OK;
+}
+
+double rtg_group_reduce_ms(rtg_group* g) { return g ? g->reduce_ms : 0.0; }
+
+int rtg_group_uses_rccl(rtg_group* g) { return g && !g->comms.empty() ? 1 : 0; }
+
+}  // extern "C"

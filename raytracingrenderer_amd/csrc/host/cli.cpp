@@ -10,10 +10,15 @@
 // -maxDepth (MAX_DEPTH, 4), -seed (sampler seed, 1234), -device, -batch (spp per rtg_render call;
 // results do not depend on it), -skipMissing 1 (filtered scene variants), -envmap <file>,
 // -timeLimit <s> (10; 0 = none).
+// Multi-GPU (one node): -gpus N renders on devices 0..N-1, -devices a,b,... on a list. Rank r
+// renders the 32x32 tiles with (tile_x + tile_y) % N == r, one host thread per device, and the films
+// are summed into the first device by one RCCL reduce before the film is written (rtg_group_*,
+// include/rtg.h); the output is bit-identical to the one-device render.
 #include "../../../include/rth.h"
 
 #include <chrono>
 #include <cstdio>
+#include <sstream>
 #include <cstdlib>
 #include <string>
 #include <unordered_map>
@@ -58,9 +63,26 @@ int main(int argc, char** argv) {
     if (rth_load_scene(scene_name.c_str(), &lo, &scene) != 0) return die("loadScene", rth_last_error());
     rth_scene_info info{};
     rth_scene_get_info(scene, &info);
+    std::vector<int> devices;
+    if (args.count("-devices")) {
+        std::stringstream ss(args["-devices"]);
+        std::string tok;
+        while (std::getline(ss, tok, ',')) devices.push_back(std::stoi(tok));
+    } else if (args.count("-gpus")) {
+        for (int i = 0; i < std::stoi(args["-gpus"]); ++i) devices.push_back(i);
+    }
     rtg_handle* rt = nullptr;
-    if (rtg_create(device, rth_scene_desc(scene), &rt) != 0) return die("rtg_create", rtg_last_error());
-    if (rtg_set_options(rt, max_depth, RTG_OPT_CULL, 0) != 0) return die("rtg_set_options", rtg_last_error());
+    rtg_group* grp = nullptr;
+    if (devices.empty()) {
+        if (rtg_create(device, rth_scene_desc(scene), &rt) != 0) return die("rtg_create", rtg_last_error());
+        if (rtg_set_options(rt, max_depth, RTG_OPT_CULL, 0) != 0) return die("rtg_set_options", rtg_last_error());
+    } else {
+        if (rtg_group_create(devices.data(), (int)devices.size(), rth_scene_desc(scene), &grp) != 0)
+            return die("rtg_group_create", rtg_last_error());
+        if (rtg_group_set_options(grp, max_depth, RTG_OPT_CULL, 0) != 0) return die("rtg_group_set_options", rtg_last_error());
+        std::printf("%d devices, film reduce by %s\n", (int)devices.size(),
+                    rtg_group_uses_rccl(grp) ? "RCCL (ncclReduce)" : "host memory (repeated devices)");
+    }
     std::printf("scene %s: %u triangles, %u lights, %dx%d (load %.0f ms, BVH %.0f ms)\n", scene_name.c_str(),
                 info.n_tris, info.n_lights, info.width, info.height, info.load_ms, info.bvh_ms);
 
@@ -69,7 +91,8 @@ int main(int argc, char** argv) {
     while (spp < spp_target) {
         const unsigned n = std::min(batch, spp_target - spp);
         auto t0 = std::chrono::steady_clock::now();
-        if (rtg_render(rt, spp, n, seed, nullptr, 0) != 0) return die("rtg_render", rtg_last_error());
+        const int rc = grp ? rtg_group_render(grp, spp, n, seed) : rtg_render(rt, spp, n, seed, nullptr, 0);
+        if (rc != 0) return die("rtg_render", rtg_last_error());
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         total += dt;
         spp += n;
@@ -78,7 +101,12 @@ int main(int argc, char** argv) {
     }
     std::vector<float> film((size_t)info.width * info.height * 3);
     uint32_t got = 0;
-    if (rtg_film_read(rt, film.data(), &got) != 0) return die("rtg_film_read", rtg_last_error());
+    if (grp) {
+        if (rtg_group_film_read(grp, film.data(), &got) != 0) return die("rtg_group_film_read", rtg_last_error());
+        std::printf("film reduce: %.3f ms\n", rtg_group_reduce_ms(grp));
+    } else if (rtg_film_read(rt, film.data(), &got) != 0) {
+        return die("rtg_film_read", rtg_last_error());
+    }
     const std::string auto_name = "result_" + std::to_string(got) + ".hdr";
     if (rth_save_hdr(auto_name.c_str(), info.width, info.height, film.data(), got) != 0)
         return die("saveHDR", rth_last_error());
@@ -90,7 +118,8 @@ int main(int argc, char** argv) {
         if (rc != 0) return die(png ? "savePNG" : "saveHDR", rth_last_error());
         std::printf("wrote %s\n", filename.c_str());
     }
-    rtg_destroy(rt);
+    if (rt) rtg_destroy(rt);
+    if (grp) rtg_group_destroy(grp);
     rth_free_scene(scene);
     return 0;
 }

@@ -302,3 +302,65 @@ class RayTracer:
         _check(self._lib.rtg_trace_visible(self._h, N.ptr(r, C.c_float), len(r), N.ptr(out, C.c_int32)),
                self._lib.rtg_last_error)
         return out
+
+
+class RayTracerGroup:
+    """RayTracer over several GPUs of one node (rtg_group_*, rtg_multi.hip): rank r renders the 32x32
+    tiles with (tile_x + tile_y) % N == r on devices[r] (one host thread per device), and film()
+    sums the films into devices[0] with one RCCL reduce. The result is bit-identical to a one-device
+    render (RayTracer::pathTracerTileBased's tile pool, Renderer.h:836-853, spread over devices).
+    A device list with repeats rehearses N ranks on fewer GPUs (the sum then goes through host
+    memory)."""
+
+    def __init__(self, scene, devices=(0,), max_depth=RayTracer.MAX_DEPTH, seed=1234, cull=True, max_paths=0):
+        self.scene = scene
+        self.seed = seed
+        self.devices = list(devices)
+        self.width, self.height = scene.width, scene.height
+        self._lib = N.rtg()
+        dev = np.ascontiguousarray(self.devices, np.int32)
+        g = C.c_void_p()
+        _check(self._lib.rtg_group_create(N.ptr(dev, C.c_int32), len(dev), scene.desc_ptr, C.byref(g)),
+               self._lib.rtg_last_error)
+        self._g = g
+        _check(self._lib.rtg_group_set_options(g, max_depth, N.RTG_OPT_CULL if cull else 0, max_paths),
+               self._lib.rtg_last_error)
+        self._spp = 0
+
+    def __del__(self):
+        g, self._g = getattr(self, "_g", None), None
+        if g:
+            self._lib.rtg_group_destroy(g)
+
+    @property
+    def uses_rccl(self):
+        return bool(self._lib.rtg_group_uses_rccl(self._g))
+
+    def render(self, n_samples=1, first_sample=None):
+        first = self._spp if first_sample is None else first_sample
+        _check(self._lib.rtg_group_render(self._g, first, n_samples, self.seed), self._lib.rtg_last_error)
+        self._spp = first + n_samples
+
+    def film(self):
+        """(sum, spp) of the reduced film."""
+        out = np.zeros((self.height, self.width, 3), np.float32)
+        spp = C.c_uint32()
+        _check(self._lib.rtg_group_film_read(self._g, N.ptr(out, C.c_float), C.byref(spp)), self._lib.rtg_last_error)
+        return out, spp.value
+
+    def reduce_ms(self):
+        return self._lib.rtg_group_reduce_ms(self._g)
+
+    def clear(self):
+        _check(self._lib.rtg_group_clear(self._g), self._lib.rtg_last_error)
+        self._spp = 0
+
+
+def tiles_for_rank_native(width, height, rank, world):
+    """rtg_tiles_for_rank (the C partition the group uses); equals distributed.tiles_for_rank."""
+    lib = N.rtg()
+    n = C.c_uint32()
+    _check(lib.rtg_tiles_for_rank(width, height, rank, world, None, C.byref(n)), lib.rtg_last_error)
+    out = np.zeros(n.value, np.uint32)
+    _check(lib.rtg_tiles_for_rank(width, height, rank, world, N.ptr(out, C.c_uint32), C.byref(n)), lib.rtg_last_error)
+    return out

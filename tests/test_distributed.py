@@ -116,3 +116,56 @@ def test_librtg_handles_sum_to_one_render(world):
         assert not f[outside].view(np.uint32).any()
         acc += f
     assert np.array_equal(acc.view(np.uint32), full.view(np.uint32))
+
+
+def test_native_tile_partition_matches_python():
+    """rtg_tiles_for_rank (librtg, used by rtg_group and the CLI's -gpus) is the partition of
+    distributed.tiles_for_rank (pure host code: no GPU needed)."""
+    from raytracingrenderer_amd.distributed import tiles_for_rank
+    from raytracingrenderer_amd.renderer import tiles_for_rank_native
+    for w, h, n in [(1024, 1024, 8), (1920, 1080, 3), (100, 50, 4), (4096, 4096, 8), (40, 40, 5)]:
+        for r in range(n):
+            assert np.array_equal(tiles_for_rank_native(w, h, r, n), tiles_for_rank(w, h, r, n))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
+def test_group_film_equals_one_device(devices):
+    """rtg_group: one device through an RCCL communicator (ncclCommInitAll + ncclReduce), or N
+    ranks rehearsed on the box's one GPU (host-memory sum): the reduced film equals one handle's
+    render of every tile, bit for bit."""
+    from raytracingrenderer_amd import RayTracer, RayTracerGroup, loadScene
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=200, height=136)
+    one = RayTracer(s, seed=31)
+    one.render(3, first_sample=0)
+    want = one.film()[0]
+    g = RayTracerGroup(s, devices=devices, seed=31)
+    assert g.uses_rccl == (len(set(devices)) == len(devices))
+    g.render(2)
+    g.render(1)
+    got, spp = g.film()
+    assert spp == 3
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    g.clear()
+    g.render(3, first_sample=0)
+    assert np.array_equal(g.film()[0].view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [["-gpus", "1"], ["-devices", "0,0,0"]])
+def test_cli_multi_gpu_output_equals_single(tmp_path, opt):
+    """The CLI's multi-GPU mode (Main.cpp frame loop on rtg_group) writes the same result_<spp>.hdr
+    bytes as the one-device CLI."""
+    import subprocess
+    from raytracingrenderer_amd import _native as N
+    cli = os.path.join(N.LIB_DIR, "rtg_render")
+    base = [cli, "-scene", os.path.join(SCENES, "cornell-box"), "-SPP", "4", "-width", "96", "-height", "64",
+            "-timeLimit", "0", "-batch", "2"]
+    (tmp_path / "one").mkdir()
+    (tmp_path / "multi").mkdir()
+    r1 = subprocess.run(base, cwd=str(tmp_path / "one"), capture_output=True, text=True, timeout=300)
+    r2 = subprocess.run(base + opt, cwd=str(tmp_path / "multi"), capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stderr
+    assert r2.returncode == 0, r2.stderr
+    assert ("RCCL" in r2.stdout) == (opt[0] == "-gpus")
+    assert (tmp_path / "one" / "result_4.hdr").read_bytes() == (tmp_path / "multi" / "result_4.hdr").read_bytes()
