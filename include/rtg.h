@@ -133,7 +133,7 @@ void rtg_destroy(rtg_handle* h);
  * RTG_OPT_COUNT runs the counting kernels (node / triangle tests in rtg_stats);
  * RTG_OPT_TIMING records HIP events around every launch (per-kernel-class ms in rtg_stats);
  * RTG_OPT_BVH2 forces the reference BVH2 walk (no 4-wide collapse; verification / A-B).
- * max_paths_in_flight bounds the paths of one wavefront chunk (0 = keep, default 256M; a chunk's path
+ * max_paths_in_flight bounds the paths of one wavefront chunk (0 = keep, default 1G; a chunk's path
  * state is also held to half the free HBM). */
 #define RTG_OPT_CULL   1
 #define RTG_OPT_COUNT  2

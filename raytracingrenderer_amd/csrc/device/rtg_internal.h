@@ -199,7 +199,7 @@ struct rtg_handle {
     int W = 0, H = 0;
     uint32_t spp = 0;
     int max_depth = 4, cull = 1, count = 0, timing = 0;
-    uint32_t max_paths = 1u << 28;  // 256M paths in flight (~63 GB at depth 4), clamped to half the free HBM
+    uint32_t max_paths = 1u << 30;  // 1G paths in flight at most; the chunk is held to half the free HBM
     int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0, shade_blocks = 0, packet_blocks = 0;
     int fetch8 = RTG_FETCH8;  // sliced work counters for k_trace (RTG_FETCH8 env overrides)
     int pixel_major = 1;  // path ids pixel-major: a wave's rays share pixels (RTG_PIXEL_MAJOR=0: sample-major)

@@ -2000,6 +2000,19 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     // fold stays in sample order: chunk c's k_accumulate waits for chunk c-1's.
     const int pipes = (h->pipes >= 2 && n_samples >= 2) ? 2 : 1;
     if (pipes == 2 && ns_chunk >= n_samples) ns_chunk = (n_samples + 1) / 2;
+    // Keep the chunk buffers once they hold most of what the budget asks for: the free-memory
+    // reading moves between calls, and growing a buffer of ~100 GB means a free and a new
+    // hipMalloc that took 5.5 s on C4 with 1G paths in flight (tools/c4_stall.sh).
+    {
+        const uint32_t fit = h->cap_maxb[0] >= planes ? (uint32_t)(h->cap_P[0] / std::max(1u, h->npix)) : 0u;
+        if (fit >= 1 && ns_chunk > fit && (uint64_t)fit * 4 >= (uint64_t)ns_chunk * 3) ns_chunk = fit;
+    }
+    // equal chunks: 256 samples at <= 123 per chunk run as 86 + 85 + 85, not 123 + 123 + 10 (a thin
+    // last chunk is mostly drain tail)
+    {
+        const uint32_t nchunks = (n_samples + ns_chunk - 1) / ns_chunk;
+        ns_chunk = (n_samples + nchunks - 1) / nchunks;
+    }
     const size_t P = (size_t)ns_chunk * h->npix;
     for (int i = 0; i < pipes; ++i)
         if ((rc = ensure_chunk(h, i, P, planes))) return rc;
