@@ -47,18 +47,20 @@ class RefScene:
         self.L.ref_counts(C.c_void_p(self.h), _p(c))
         self.ntri, self.nnode, self.nlight, self.nmat, self.ntex, self.env_tex, self.W, self.H = c.tolist()
 
-    def render(self, n_samples, first=0, seed=1234, max_depth=4, threads=8, film=None, count=False):
+    def render(self, n_samples, first=0, seed=1234, max_depth=4, threads=8, film=None, count=False, mode=0):
         """ref_render: RayTracer::render x n_samples on the reference's own classes (tile pool of
-        `threads` std::threads, deterministic sampler). Returns (film sum, counts[paths, closest,
-        shadow])."""
+        `threads` std::threads, deterministic sampler). mode: 0 pathTrace, 1 direct, 2 albedo,
+        3 viewNormals, 4 direct with computeDirectMIS (RTG_INTEGRATOR_*). Returns (film sum,
+        counts[paths, closest, shadow])."""
         if film is None:
             film = np.zeros((self.H, self.W, 3), np.float32)
         counts = np.zeros(3, np.uint64)
         L = self.L
-        L.ref_render.restype = C.c_int
-        L.ref_render.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.c_void_p,
-                                 C.c_void_p]
-        L.ref_render(self.h, first, n_samples, seed, max_depth, threads, film.ctypes.data, counts.ctypes.data)
+        L.ref_render_mode.restype = C.c_int
+        L.ref_render_mode.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.c_void_p,
+                                      C.c_void_p, C.c_int]
+        L.ref_render_mode(self.h, first, n_samples, seed, max_depth, threads, film.ctypes.data, counts.ctypes.data,
+                          mode)
         return film, counts
 
     def export(self):
@@ -152,3 +154,41 @@ def tonemap(film_sum, spp, exposure=1.0):
     L.ref_tonemap.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_float, C.c_void_p]
     L.ref_tonemap(f.shape[1], f.shape[0], f.ctypes.data, spp, C.c_float(exposure), out.ctypes.data)
     return out
+
+
+def _bind_extra(L):
+    if getattr(L, "_extra_bound", False):
+        return L
+    L.ref_render_light.restype = C.c_int
+    L.ref_render_light.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p]
+    L.ref_render_ir.restype = C.c_int
+    L.ref_render_ir.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_void_p]
+    L.ref_render_adaptive.restype = C.c_int
+    L.ref_render_adaptive.argtypes = [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.c_void_p, C.c_void_p]
+    L._extra_bound = True
+    return L
+
+
+def render_light(ref_scene, n_frames=1, first=0, seed=1234):
+    """RayTracer::lightTracer restated on the reference's classes (ref_render_light)."""
+    film = np.zeros((ref_scene.H, ref_scene.W, 3), np.float32)
+    _bind_extra(ref_scene.L).ref_render_light(ref_scene.h, first, n_frames, seed, film.ctypes.data)
+    return film
+
+
+def render_instant_radiosity(ref_scene, n_frames=1, first=0, seed=1234, n_vpl=50):
+    """RayTracer::instantRadiosity restated on the reference's classes (ref_render_ir)."""
+    film = np.zeros((ref_scene.H, ref_scene.W, 3), np.float32)
+    _bind_extra(ref_scene.L).ref_render_ir(ref_scene.h, first, n_frames, seed, n_vpl, film.ctypes.data)
+    return film
+
+
+def render_adaptive(ref_scene, first=0, seed=1234, init=2, max_samples=10240, min_samples=1):
+    """RayTracer::adaptiveRender restated on the reference's classes (ref_render_adaptive)."""
+    film = np.zeros((ref_scene.H, ref_scene.W, 3), np.float32)
+    nt = ((ref_scene.W + 31) // 32) * ((ref_scene.H + 31) // 32)
+    counts = np.zeros(nt, np.uint32)
+    _bind_extra(ref_scene.L).ref_render_adaptive(ref_scene.h, first, seed, init, max_samples, min_samples,
+                                                 film.ctypes.data, counts.ctypes.data)
+    return film, counts

@@ -60,6 +60,7 @@ template <class T> inline T win_min(T a, T b) { return a < b ? a : b; }
 template <class T> inline T win_max(T a, T b) { return a > b ? a : b; }
 
 struct RayCount { uint64_t ext = 0, shadow = 0; };
+const int MAX_DEPTH_REF = 4;  // Renderer.h:20 (the adaptive renderer uses the reference default)
 
 // RayTracer::computeDirect (Renderer.h:423-473) on the reference classes
 Colour ref_compute_direct(Scene* scene, ShadingData shadingData, Sampler& sampler, RayCount& rc) {
@@ -115,6 +116,192 @@ Colour ref_path_trace(Scene* scene, Ray& r, Colour& thr, int depth, int max_dept
         return (direct + ref_path_trace(scene, r, thr, depth + 1, max_depth, sampler, shadingData.bsdf->isPureSpecular(), rc));
     }
     return scene->background->evaluate(r.dir);
+}
+
+float balance_heuristic(float a, float b) { return a / (a + b); }  // Renderer.h:408-411
+float area_to_solid(float pdf_area, float dist2, float costheta) {  // Renderer.h:412-422
+    if (costheta > 0.0f) return pdf_area * dist2 / costheta;
+    return 0.0f;
+}
+
+// RayTracer::computeDirectMIS (Renderer.h:474-557)
+Colour ref_compute_direct_mis(Scene* scene, ShadingData shadingData, Sampler& sampler, RayCount& rc) {
+    if (shadingData.bsdf->isPureSpecular() == true) return Colour(0.0f, 0.0f, 0.0f);
+    Colour result(0.0f, 0.0f, 0.0f);
+    float pmf;
+    Light* light = scene->sampleLight(sampler, pmf);
+    float pdf;
+    Colour emitted;
+    Vec3 p = light->sample(shadingData, sampler, emitted, pdf);
+    if (light->isArea()) {
+        Vec3 wi = p - shadingData.x;
+        float l = wi.lengthSq();
+        wi = wi.normalize();
+        float cos_surface = win_max(Dot(wi, shadingData.sNormal), 0.0f);
+        float cos_light = win_max(-Dot(wi, light->normal(shadingData, wi)), 0.0f);
+        float g = cos_surface * cos_light / l;
+        if (g > 0) {
+            rc.shadow++;
+            if (scene->visible(shadingData.x, p)) {
+                float pdf_bsdf = shadingData.bsdf->PDF(shadingData, wi);
+                float pdf_light = area_to_solid(pdf * pmf, l, cos_light);
+                float weight = balance_heuristic(pdf_light, pdf_bsdf);
+                result = result + shadingData.bsdf->evaluate(shadingData, wi) * emitted * g * weight / (pmf * pdf);
+            }
+        }
+    } else {
+        Vec3 wi = p;
+        float g = win_max(Dot(wi, shadingData.sNormal), 0.0f);
+        if (g > 0) {
+            rc.shadow++;
+            if (scene->visible(shadingData.x, shadingData.x + (p * 10000.0f)))
+                return shadingData.bsdf->evaluate(shadingData, wi) * emitted * g / (pmf * pdf);
+        }
+    }
+    Colour val_bsdf;
+    float pdf_bsdf;
+    Vec3 wi_bsdf = shadingData.bsdf->sample(shadingData, sampler, val_bsdf, pdf_bsdf);
+    Ray r = Ray(shadingData.x + (wi_bsdf * EPSILON), wi_bsdf);
+    rc.ext++;
+    IntersectionData intersection = scene->traverse(r);
+    ShadingData hit = scene->calculateShadingData(intersection, r);
+    if (hit.t < FLT_MAX) {
+        if (hit.bsdf->isLight()) {
+            Colour emitted2 = hit.bsdf->emit(hit, -wi_bsdf);
+            Vec3 wi = hit.x - shadingData.x;
+            float dist2 = wi.lengthSq();
+            wi = wi.normalize();
+            float cos_light = win_max(0.0f, Dot(-wi, hit.sNormal));
+            float pdf_light = area_to_solid(pdf * pmf, dist2, cos_light);
+            float weight = balance_heuristic(pdf_bsdf, pdf_light);
+            result = result + val_bsdf * emitted2 * win_max(0.0f, Dot(wi_bsdf, shadingData.sNormal)) * weight / pdf_bsdf;
+        }
+    }
+    return result;
+}
+
+// The per-pixel estimators of RayTracer (Renderer.h:393-407 direct, :558-571 albedo, :572-582
+// viewNormals; mode 4 = direct() with computeDirectMIS); mode 0 is pathTrace.
+Colour ref_estimate(Scene* scene, Ray& r, int mode, int max_depth, Sampler& sampler, RayCount& rc) {
+    if (mode == 0) {
+        Colour thr(1.0f, 1.0f, 1.0f);
+        return ref_path_trace(scene, r, thr, 0, max_depth, sampler, true, rc);
+    }
+    rc.ext++;
+    IntersectionData intersection = scene->traverse(r);
+    if (mode == 3) {
+        if (intersection.t < FLT_MAX) {
+            ShadingData sd = scene->calculateShadingData(intersection, r);
+            return Colour(fabsf(sd.sNormal.x), fabsf(sd.sNormal.y), fabsf(sd.sNormal.z));
+        }
+        return Colour(0.0f, 0.0f, 0.0f);
+    }
+    ShadingData sd = scene->calculateShadingData(intersection, r);
+    if (sd.t < FLT_MAX) {
+        if (sd.bsdf->isLight()) return sd.bsdf->emit(sd, sd.wo);
+        if (mode == 2) return sd.bsdf->evaluate(sd, Vec3(0, 1, 0));
+        return mode == 4 ? ref_compute_direct_mis(scene, sd, sampler, rc) : ref_compute_direct(scene, sd, sampler, rc);
+    }
+    if (mode == 2) return scene->background->evaluate(r.dir);
+    return Colour(0.0f, 0.0f, 0.0f);
+}
+
+// ---- light tracing (Renderer.h:221-326), restated on the reference classes. `film` is the
+// reference's Film; splats happen in path and vertex order (the reference's loop is sequential).
+void ref_connect_to_camera(Scene* scene, Film& film, Vec3 p, Vec3 n, Colour col) {  // :236-262
+    float x, y;
+    if (scene->camera.projectOntoCamera(p, x, y)) {
+        float A_film = scene->camera.Afilm;
+        Vec3 direction = scene->camera.origin - p;
+        float dist2 = direction.lengthSq();
+        direction = direction.normalize();
+        float cos_theta_shading = Dot(n, direction);
+        float cos_theta_cam = Dot(scene->camera.viewDirection, -direction);
+        if (cos_theta_shading < 0.0f || cos_theta_cam < 0.0f) return;
+        float G = (cos_theta_shading * cos_theta_cam) / dist2;
+        if (!scene->visible(p, scene->camera.origin)) return;
+        float W_e = 1 / (A_film * SQ(SQ(cos_theta_cam)));
+        Colour color = col * W_e * G;
+        film.splat(x, y, color);
+    }
+}
+void ref_light_trace_path(Scene* scene, Film& film, Ray& r, Colour thr, Colour Le, Sampler& sampler) {  // :292-326
+    for (;;) {
+        IntersectionData intersection = scene->traverse(r);
+        ShadingData sd = scene->calculateShadingData(intersection, r);
+        if (!(sd.t < FLT_MAX)) return;
+        if (sd.bsdf->isLight() || sd.bsdf->isPureSpecular()) return;
+        Vec3 wi = scene->camera.origin - sd.x;
+        wi = wi.normalize();
+        Colour col = thr * sd.bsdf->evaluate(sd, wi) * Le;
+        ref_connect_to_camera(scene, film, sd.x, sd.sNormal, col);
+        float rrp = win_min(thr.Lum(), 0.9f);
+        if (sampler.next() < rrp) thr = thr / rrp;
+        else return;
+        Colour indirect;
+        float pdf;
+        Vec3 wi2 = sd.bsdf->sample(sd, sampler, indirect, pdf);
+        thr = thr * indirect * fabsf(Dot(wi2, sd.sNormal)) / pdf;
+        r.init(sd.x + (wi2 * EPSILON), wi2);
+    }
+}
+void ref_light_trace_init(Scene* scene, Film& film, Sampler& sampler) {  // :264-291
+    float pmf;
+    Light* light = scene->sampleLight(sampler, pmf);
+    if (!light->isArea()) return;
+    float pdfPosition, pdfDirection;
+    Vec3 p = light->samplePositionFromLight(sampler, pdfPosition);
+    Vec3 wi = light->sampleDirectionFromLight(sampler, pdfDirection);
+    ShadingData tmp;
+    Vec3 lightNormal = light->normal(tmp, wi);
+    float cosTheta = Dot(lightNormal, wi);
+    Colour Le = light->evaluate(-wi) * cosTheta / (pmf * pdfDirection * pdfPosition);
+    ref_connect_to_camera(scene, film, p, lightNormal, Le);
+    Ray r = Ray(p, wi);
+    ref_light_trace_path(scene, film, r, Colour(1.0f, 1.0f, 1.0f), Le, sampler);
+}
+
+// ---- instant radiosity (Renderer.h:82-218)
+struct RefVpl { ShadingData shadingData; Colour Le; };
+void ref_vpl_trace_path(Scene* scene, Ray& r, Colour thr, Colour Le, Sampler& sampler, std::vector<RefVpl>& vpls) {
+    for (;;) {  // VPLTracePath, :183-218
+        IntersectionData intersection = scene->traverse(r);
+        ShadingData sd = scene->calculateShadingData(intersection, r);
+        if (!(sd.t < FLT_MAX)) return;
+        if (!sd.bsdf->isLight() && !sd.bsdf->isPureSpecular()) {
+            RefVpl v;
+            v.shadingData = sd;
+            v.Le = thr * Le * sd.bsdf->evaluate(sd, -r.dir) * fabsf(Dot(-r.dir, sd.sNormal));
+            vpls.push_back(v);
+        }
+        float rrp = win_min(thr.Lum(), 0.9f);
+        if (sampler.next() < rrp) thr = thr / rrp;
+        else return;
+        Colour bsdfVal;
+        float pdf;
+        Vec3 wi = sd.bsdf->sample(sd, sampler, bsdfVal, pdf);
+        thr = thr * bsdfVal * fabsf(Dot(wi, sd.sNormal)) / pdf;
+        r.init(sd.x + (wi * EPSILON), wi);
+    }
+}
+Colour ref_vpl_contribution(Scene* scene, ShadingData sd, const std::vector<RefVpl>& vpls) {  // :122-154
+    if (sd.bsdf->isLight() || sd.bsdf->isPureSpecular()) return Colour(0.0f, 0.0f, 0.0f);
+    Colour col_sum(0.0f, 0.0f, 0.0f);
+    for (const RefVpl& vpl : vpls) {
+        Vec3 direction = vpl.shadingData.x - sd.x;
+        float dist2 = direction.lengthSq();
+        if (dist2 < 1e-4f) continue;
+        direction = direction.normalize();
+        float cos_theta_vpl = Dot(vpl.shadingData.sNormal, -direction);
+        float cos_theta_x = Dot(sd.sNormal, direction);
+        if (cos_theta_vpl <= 0.0f || cos_theta_x <= 0.0f) continue;
+        float G = (cos_theta_vpl * cos_theta_x) / dist2;
+        if (!scene->visible(sd.x, vpl.shadingData.x)) continue;
+        Colour bsdf = sd.bsdf->evaluate(sd, direction);
+        Colour col = vpl.Le * bsdf * G;
+        col_sum = col_sum + col;
+    }
+    return col_sum;
 }
 
 bool exists(const std::string& p) {
@@ -480,8 +667,8 @@ int ref_save_hdr(const char* path, int w, int h, const float* sum, int spp) {
 // and splat every pixel's pathTrace radiance into the reference's Film (box filter). The film sum
 // (w*h*3, in/out) and the deterministic sampler replace MTRandom. counts (optional, 3): paths,
 // closest-hit rays, shadow rays.
-int ref_render(void* h, uint32_t first, uint32_t n_samples, uint64_t seed, int max_depth, int threads, float* sum,
-               uint64_t* counts) {
+int ref_render_mode(void* h, uint32_t first, uint32_t n_samples, uint64_t seed, int max_depth, int threads, float* sum,
+                    uint64_t* counts, int mode) {
     RefScene* rs = (RefScene*)h;
     Scene* scene = rs->scene;
     const int W = (int)scene->camera.width, H = (int)scene->camera.height, TS = 32;
@@ -504,8 +691,7 @@ int ref_render(void* h, uint32_t first, uint32_t n_samples, uint64_t seed, int m
                         float px = x + 0.5f, py = y + 0.5f;
                         PcgSampler sampler(seed, ((uint64_t)(y * W + x) << 16) | smp);
                         Ray ray = scene->camera.generateRay(px, py);
-                        Colour thr(1.0f, 1.0f, 1.0f);
-                        Colour col = ref_path_trace(scene, ray, thr, 0, max_depth, sampler, true, rcs[tid]);
+                        Colour col = ref_estimate(scene, ray, mode, max_depth, sampler, rcs[tid]);
                         film.splat(px, py, col);
                     }
             }
@@ -520,6 +706,134 @@ int ref_render(void* h, uint32_t first, uint32_t n_samples, uint64_t seed, int m
         counts[1] = counts[2] = 0;
         for (auto& c : rcs) { counts[1] += c.ext; counts[2] += c.shadow; }
     }
+    return 0;
+}
+
+int ref_render(void* h, uint32_t first, uint32_t n_samples, uint64_t seed, int max_depth, int threads, float* sum,
+               uint64_t* counts) {
+    return ref_render_mode(h, first, n_samples, seed, max_depth, threads, sum, counts, 0);
+}
+
+// RayTracer::lightTracer (Renderer.h:221-235): width*height light paths per frame, path i of frame f
+// drawing from the PCG stream keyed (seed, i << 16 | f) (the GPU build's convention).
+int ref_render_light(void* h, uint32_t first, uint32_t n_frames, uint64_t seed, float* sum) {
+    Scene* scene = ((RefScene*)h)->scene;
+    const int W = (int)scene->camera.width, H = (int)scene->camera.height;
+    Film film;
+    film.init(W, H, new BoxFilter());
+    memcpy(film.film, sum, (size_t)W * H * 12);
+    for (uint32_t f = first; f < first + n_frames; ++f)
+        for (uint32_t i = 0; i < (uint32_t)(W * H); ++i) {
+            PcgSampler sampler(seed, ((uint64_t)i << 16) | f);
+            ref_light_trace_init(scene, film, sampler);
+        }
+    memcpy(sum, film.film, (size_t)W * H * 12);
+    return 0;
+}
+
+// RayTracer::instantRadiosity (Renderer.h:101-121): traceVPLs (n_vpl paths, path i keyed (seed,
+// i << 16 | f)), then every pixel's first hit gathers the VPLs (renderBlockinstantRadiosity).
+int ref_render_ir(void* h, uint32_t first, uint32_t n_frames, uint64_t seed, uint32_t n_vpl, float* sum) {
+    Scene* scene = ((RefScene*)h)->scene;
+    const int W = (int)scene->camera.width, H = (int)scene->camera.height;
+    Film film;
+    film.init(W, H, new BoxFilter());
+    memcpy(film.film, sum, (size_t)W * H * 12);
+    for (uint32_t f = first; f < first + n_frames; ++f) {
+        std::vector<RefVpl> vpls;
+        for (uint32_t i = 0; i < n_vpl; ++i) {  // traceVPLs, :156-182
+            PcgSampler sampler(seed, ((uint64_t)i << 16) | f);
+            float pmf;
+            Light* light = scene->sampleLight(sampler, pmf);
+            if (!light->isArea()) continue;
+            float pdfPosition, pdfDirection;
+            Vec3 p = light->samplePositionFromLight(sampler, pdfPosition);
+            Vec3 wi = light->sampleDirectionFromLight(sampler, pdfDirection);
+            RefVpl v;
+            ShadingData tmp;
+            v.shadingData = ShadingData(p, light->normal(tmp, p));
+            v.Le = light->evaluate(-wi) / (pmf * pdfPosition * (float)n_vpl);
+            vpls.push_back(v);
+            Colour Le = light->evaluate(-wi) * Dot(wi, light->normal(tmp, p)) / (pmf * pdfPosition * (float)n_vpl);
+            Ray r = Ray(p, wi);
+            ref_vpl_trace_path(scene, r, Colour(1.0f, 1.0f, 1.0f), Le, sampler, vpls);
+        }
+        for (int y = 0; y < H; y++)
+            for (int x = 0; x < W; x++) {
+                Ray r = scene->camera.generateRay(x + 0.5f, y + 0.5f);
+                IntersectionData intersection = scene->traverse(r);
+                ShadingData sd = scene->calculateShadingData(intersection, r);
+                if (sd.t < FLT_MAX) film.splat((float)x, (float)y, ref_vpl_contribution(scene, sd, vpls));
+            }
+    }
+    memcpy(sum, film.film, (size_t)W * H * 12);
+    return 0;
+}
+
+// RayTracer::adaptiveRender (Renderer.h:583-749): adaptiveSampling per tile (init samples per pixel,
+// variance of the per-pixel means), weights = variance / total, sampleTileWithWeight. Sample
+// indices: pass 1 first .. first+init-1, pass 2 first+init ... (the GPU build's convention).
+int ref_render_adaptive(void* h, uint32_t first, uint64_t seed, uint32_t init, uint32_t max_samples,
+                        uint32_t min_samples, float* sum, uint32_t* tile_samples) {
+    Scene* scene = ((RefScene*)h)->scene;
+    const int W = (int)scene->camera.width, H = (int)scene->camera.height, TS = 32;
+    const int tx = (W + TS - 1) / TS, ty = (H + TS - 1) / TS;
+    Film film;
+    film.init(W, H, new BoxFilter());
+    memcpy(film.film, sum, (size_t)W * H * 12);
+    RayCount rc;
+    std::vector<float> var(tx * ty);
+    for (int t = 0; t < tx * ty; ++t) {  // adaptiveSampling, :583-638
+        int startX = (t % tx) * TS, startY = (t / tx) * TS;
+        int endX = win_min(startX + TS, W), endY = win_min(startY + TS, H);
+        std::vector<Colour> est((endX - startX) * (endY - startY), Colour(0.0f, 0.0f, 0.0f));
+        int pixelIndex = 0;
+        for (int y = startY; y < endY; y++)
+            for (int x = startX; x < endX; x++) {
+                Colour s0(0.0f, 0.0f, 0.0f);
+                for (uint32_t i = 0; i < init; i++) {
+                    PcgSampler sampler(seed, ((uint64_t)(y * W + x) << 16) | (first + i));
+                    Ray ray = scene->camera.generateRay(x + 0.5f, y + 0.5f);
+                    Colour thr(1.0f, 1.0f, 1.0f);
+                    s0 = s0 + ref_path_trace(scene, ray, thr, 0, MAX_DEPTH_REF, sampler, true, rc);
+                }
+                est[pixelIndex++] = s0 / (float)init;
+            }
+        Colour es(0.0f, 0.0f, 0.0f);
+        for (size_t i = 0; i < est.size(); i++) es = es + est[i];
+        Colour gt = es / (float)pixelIndex;
+        Colour sq(0.0f, 0.0f, 0.0f);
+        for (size_t i = 0; i < est.size(); i++) {
+            Colour tmp = est[i] - gt;
+            sq = sq + tmp * tmp;
+        }
+        var[t] = ((sq.r + sq.g + sq.b) / 3.0f) / (float)(pixelIndex - 1);
+    }
+    float total = 0.0f;
+    for (float v : var) total += v;
+    for (int t = 0; t < tx * ty; ++t) {  // sampleTileWithWeight, :640-672
+        float weight = (total > 0.0f) ? var[t] / total : 0.0f;
+        weight = sqrt(weight);
+        int sample = (int)(weight * max_samples);
+        sample = win_max(sample, (int)min_samples);
+        if (tile_samples) tile_samples[t] = (uint32_t)sample;
+        int startX = (t % tx) * TS, startY = (t / tx) * TS;
+        int endX = win_min(startX + TS, W), endY = win_min(startY + TS, H);
+        for (int y = startY; y < endY; y++)
+            for (int x = startX; x < endX; x++) {
+                float px = x + 0.5f, py = y + 0.5f;
+                Colour col(0.0f, 0.0f, 0.0f);
+                for (int i = 0; i < sample; i++) {
+                    PcgSampler sampler(seed, ((uint64_t)(y * W + x) << 16) | (first + init + (uint32_t)i));
+                    Ray ray = scene->camera.generateRay(px, py);
+                    Colour thr(1.0f, 1.0f, 1.0f);
+                    col = col + ref_path_trace(scene, ray, thr, 0, MAX_DEPTH_REF, sampler, true, rc);
+                }
+                col = col / (float)sample;
+                film.splat(px, py, col);
+            }
+    }
+    memcpy(sum, film.film, (size_t)W * H * 12);
     return 0;
 }
 

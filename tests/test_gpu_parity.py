@@ -498,3 +498,31 @@ def test_gpu_film_vs_reference_classes(case, synth20k):
     ref, _ = r.render(spp, seed=seed, max_depth=depth, threads=8)
     s = loadScene(path, **kw)
     assert_bitexact(gpu_film(s, spp, seed=seed, max_depth=depth), ref, "GPU vs reference classes (%s)" % case)
+
+
+@pytest.mark.parametrize("scene_name", ["cornell-box", "cornell-mat"])
+def test_gpu_integrators_vs_reference_classes(scene_name):
+    """f4 at the film level without the C oracle: the GPU's direct / albedo / viewNormals /
+    computeDirectMIS estimators, light tracer, instant radiosity and adaptive renderer against the
+    same integrators restated on RTBase's own compiled classes (libref_rtm.so), bit for bit."""
+    from oracle import pyref
+    if not pyref.available():
+        pytest.fail("oracle/_ref (libref_rtm.so) missing: build it where /root/reference exists")
+    path = os.path.join(SCENES, scene_name)
+    s = loadScene(path, width=64, height=48)
+    r = pyref.RefScene(path, 64, 48, False, flavour="rtm")
+    for name, mode in (("direct", 1), ("albedo", 2), ("normals", 3), ("direct_mis", 4)):
+        rt = RayTracer(s, seed=7, integrator=name)
+        rt.render(3, first_sample=0)
+        assert_bitexact(rt.film()[0], r.render(3, seed=7, max_depth=4, mode=mode)[0], name)
+    rt = RayTracer(s, seed=5)
+    rt.lightTracer(2, first_frame=0)
+    assert_bitexact(rt.film()[0], pyref.render_light(r, 2, seed=5), "light tracer")
+    rt = RayTracer(s, seed=9)
+    rt.instantRadiosity(2, n_vpl=20, first_frame=0)
+    assert_bitexact(rt.film()[0], pyref.render_instant_radiosity(r, 2, seed=9, n_vpl=20), "instant radiosity")
+    rt = RayTracer(s, seed=11)
+    counts = rt.adaptiveRender(init_samples=2, max_samples=12, min_samples=1, first_sample=0)
+    fa, ca = pyref.render_adaptive(r, seed=11, init=2, max_samples=12)
+    assert counts.tolist() == ca.tolist()
+    assert_bitexact(rt.film()[0], fa, "adaptive")

@@ -187,3 +187,30 @@ def test_c1_known_answer_from_reference_classes():
     film, c = r.render(4, seed=1234, max_depth=4, threads=8)
     assert hashlib.md5((film / np.float32(4)).astype(np.float32).tobytes()).hexdigest() == "2fe4126eaf3a9c654e6beea0a1da9ba9"
     assert c.tolist() == [262144, 702961, 429793]
+
+
+@pytest.mark.parametrize("scene_name", ["cornell-box", "cornell-mat"])
+def test_oracle_integrators_equal_reference_classes(scene_name):
+    """f4: every alternative integrator of the oracle (direct, albedo, viewNormals, computeDirectMIS,
+    lightTracer, instantRadiosity, adaptiveRender; Renderer.h:82-326, 393-749) against the same
+    integrator restated on RTBase's own compiled classes (oracle/_ref), with glibc and with the
+    shared transcendentals: films (and adaptive tile counts) identical bit for bit."""
+    from oracle import pyref
+    if not pyref.available():
+        pytest.skip("oracle/_ref not built")
+    path = os.path.join(SCENES, scene_name)
+    s = loadScene(path, width=64, height=48)
+    for fl in ("libm", "rtm"):
+        r = pyref.RefScene(path, 64, 48, False, flavour=fl)
+        for mode in (1, 2, 3, 4):
+            a, ca = r.render(3, seed=7, max_depth=4, mode=mode)
+            b, cb = Oracle(s, 4, fl, integrator=mode).render(3, seed=7, threads=8, count=True)
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (fl, mode)
+            assert ca.tolist() == cb[:3].tolist()
+        o = Oracle(s, 4, fl)
+        assert np.array_equal(pyref.render_light(r, 2, seed=5).view(np.uint32), o.render_light(2, seed=5).view(np.uint32))
+        assert np.array_equal(pyref.render_instant_radiosity(r, 2, seed=9, n_vpl=20).view(np.uint32),
+                              o.render_instant_radiosity(2, seed=9, n_vpl=20).view(np.uint32))
+        fa, ca = pyref.render_adaptive(r, seed=11, init=2, max_samples=12)
+        fb, cb = o.render_adaptive(seed=11, init=2, max_samples=12)
+        assert ca.tolist() == cb.tolist() and np.array_equal(fa.view(np.uint32), fb.view(np.uint32))
