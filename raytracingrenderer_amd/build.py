@@ -65,7 +65,7 @@ def build_device(force=False):
     src = [os.path.join(CSRC, s) for s in DEVICE_SRC]
     if force or _newer(out, _deps(src)):
         _run([HIPCC, "--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-std=c++17",
-              "-fPIC", "-shared", "-o", out] + src + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
+              "-fPIC", "-shared", "-o", out] + src + ["-ldl", "-Wl,-rpath,/opt/rocm/lib"])
     return out
 
 

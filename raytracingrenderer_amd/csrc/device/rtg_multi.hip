@@ -11,15 +11,57 @@
 //
 // A device list that repeats a device (rehearsing N ranks on one GPU) cannot form an RCCL
 // communicator; the films are then summed through host memory in rank order (same bits).
+//
+// RCCL is opened with dlopen when a group first needs a communicator (not linked into librtg):
+// a process that also loads PyTorch gets PyTorch's bundled RCCL (same soname) instead of a second
+// copy, and librtg never pulls RCCL into processes that do not use groups.
 #include "rtg_internal.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
+
+namespace {
+struct Rccl {
+    bool tried = false, ok = false;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+Rccl g_rccl;
+std::mutex g_rccl_mu;
+
+bool load_rccl() {
+    std::lock_guard<std::mutex> lock(g_rccl_mu);
+    if (g_rccl.tried) return g_rccl.ok;
+    g_rccl.tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        g_err = std::string("RCCL not found: ") + dlerror();
+        return false;
+    }
+    g_rccl.comm_init_all = (decltype(g_rccl.comm_init_all))dlsym(h, "ncclCommInitAll");
+    g_rccl.comm_destroy = (decltype(g_rccl.comm_destroy))dlsym(h, "ncclCommDestroy");
+    g_rccl.reduce = (decltype(g_rccl.reduce))dlsym(h, "ncclReduce");
+    g_rccl.group_start = (decltype(g_rccl.group_start))dlsym(h, "ncclGroupStart");
+    g_rccl.group_end = (decltype(g_rccl.group_end))dlsym(h, "ncclGroupEnd");
+    g_rccl.error_string = (decltype(g_rccl.error_string))dlsym(h, "ncclGetErrorString");
+    g_rccl.ok = g_rccl.comm_init_all && g_rccl.comm_destroy && g_rccl.reduce && g_rccl.group_start &&
+                g_rccl.group_end && g_rccl.error_string;
+    if (!g_rccl.ok) g_err = "RCCL: missing symbols";
+    return g_rccl.ok;
+}
+}  // namespace
 
 struct rtg_group {
     std::vector<int> devices;
@@ -53,7 +95,7 @@ int rtg_tiles_for_rank(uint32_t width, uint32_t height, int rank, int world, uin
 
 void rtg_group_destroy(rtg_group* g) {
     if (!g) return;
-    for (ncclComm_t c : g->comms) (void)ncclCommDestroy(c);
+    for (ncclComm_t c : g->comms) (void)g_rccl.comm_destroy(c);
     if (g->d_sum) {
         (void)hipSetDevice(g->devices[0]);
         (void)hipFree(g->d_sum);
@@ -89,11 +131,15 @@ int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* de
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
     if (distinct) {
+        if (!load_rccl()) {
+            rtg_group_destroy(g);
+            return RTG_ERR_HIP;
+        }
         g->comms.resize(n_devices);
-        const ncclResult_t nr = ncclCommInitAll(g->comms.data(), n_devices, g->devices.data());
+        const ncclResult_t nr = g_rccl.comm_init_all(g->comms.data(), n_devices, g->devices.data());
         if (nr != ncclSuccess) {
             g->comms.clear();
-            g_err = std::string("ncclCommInitAll: ") + ncclGetErrorString(nr);
+            g_err = std::string("ncclCommInitAll: ") + g_rccl.error_string(nr);
             rtg_group_destroy(g);
             return RTG_ERR_HIP;
         }
@@ -161,19 +207,19 @@ int rtg_group_reduce(rtg_group* g) {
     HIPOK(hipEventRecord(e0, g->h[0]->stream));
     if (!g->comms.empty()) {
         // every rank's film (summed in sample order on its device) -> device 0, ncclSum
-        if (ncclGroupStart() != ncclSuccess) { g_err = "ncclGroupStart failed"; return RTG_ERR_HIP; }
+        if (g_rccl.group_start() != ncclSuccess) { g_err = "ncclGroupStart failed"; return RTG_ERR_HIP; }
         for (size_t r = 0; r < n; ++r) {
             HIPOK(hipSetDevice(g->devices[r]));
-            const ncclResult_t nr = ncclReduce(g->h[r]->d_film, r == 0 ? g->d_sum : nullptr, count, ncclFloat, ncclSum, 0,
-                                               g->comms[r], g->h[r]->stream);
+            const ncclResult_t nr = g_rccl.reduce(g->h[r]->d_film, r == 0 ? g->d_sum : nullptr, count, ncclFloat, ncclSum,
+                                                  0, g->comms[r], g->h[r]->stream);
             if (nr != ncclSuccess) {
-                (void)ncclGroupEnd();
-                g_err = std::string("ncclReduce: ") + ncclGetErrorString(nr);
+                (void)g_rccl.group_end();
+                g_err = std::string("ncclReduce: ") + g_rccl.error_string(nr);
                 return RTG_ERR_HIP;
             }
         }
-        const ncclResult_t nr = ncclGroupEnd();
-        if (nr != ncclSuccess) { g_err = std::string("ncclGroupEnd: ") + ncclGetErrorString(nr); return RTG_ERR_HIP; }
+        const ncclResult_t nr = g_rccl.group_end();
+        if (nr != ncclSuccess) { g_err = std::string("ncclGroupEnd: ") + g_rccl.error_string(nr); return RTG_ERR_HIP; }
         for (size_t r = 0; r < n; ++r) {
             HIPOK(hipSetDevice(g->devices[r]));
             HIPOK(hipStreamSynchronize(g->h[r]->stream));
