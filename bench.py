@@ -144,6 +144,7 @@ def main():
             if backend == "nccl":
                 torch.cuda.synchronize()  # the previous step's reduce is done with film_t
                 rt.copy_film_to(film_t.data_ptr())
+                rt.synchronize()  # the copy runs on librtg's stream, the reduce on RCCL's
             else:
                 film_t.copy_(torch.from_numpy(rt.film()[0]))
             reduce_film(film_t, dist)
