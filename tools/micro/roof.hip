@@ -16,6 +16,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 __device__ inline unsigned hash(unsigned x) {
@@ -23,23 +24,45 @@ __device__ inline unsigned hash(unsigned x) {
     return x;
 }
 
-template <int VALU>
+template <int VALU, int LOADS = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6)))
 void k_chain(const float4* __restrict__ tab, unsigned nrec, int steps, float* out) {
     const unsigned gid = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned idx = hash(gid * 2654435761u + 12345u) % nrec;
     float acc = 0.f;
     for (int s = 0; s < steps; ++s) {
-        const float4* r = tab + (size_t)idx * 4;
-        const float4 a = r[0], b = r[1], c = r[2], d = r[3];
-        float sum = (((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w))) +
-                    (((c.x + c.y) + (c.z + c.w)) + ((d.x + d.y) + (d.z + d.w)));
+        const float4* r = tab + (size_t)idx * LOADS;
+        float4 v[LOADS];
+#pragma unroll
+        for (int k = 0; k < LOADS; ++k) v[k] = r[k];
+        const float4 a = v[0];
+        float sum = 0.0f;
+#pragma unroll
+        for (int k = 0; k < LOADS; ++k) sum += (v[k].x + v[k].y) + (v[k].z + v[k].w);
 #pragma unroll
         for (int v = 0; v < VALU; ++v) sum = __builtin_fmaf(sum, 1.0000001f, a.y * (float)v);
         acc += sum;
         idx = hash(idx ^ __float_as_uint(sum)) % nrec;
     }
     out[gid] = acc;
+}
+
+template <int LOADS>
+static double run_l(const float4* d, unsigned nrec, float* out, int blocks, int steps, int reps) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    float best = 1e30f;
+    for (int rep = 0; rep < reps; ++rep) {
+        (void)hipEventRecord(a);
+        hipLaunchKernelGGL((k_chain<64, LOADS>), dim3(blocks), dim3(256), 0, 0, d, nrec, steps, out);
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, a, b);
+        if (ms < best) best = ms;
+    }
+    return best;
 }
 
 static double run(int valu, const float4* d, unsigned nrec, float* out, int blocks, int steps, int reps) {
@@ -94,6 +117,21 @@ int main(int argc, char** argv) {
                     lanes * steps * 64.0 / ms / 1e6);
         std::fflush(stdout);
     };
+    if (argc == 2 && std::string(argv[1]) == "width") {
+        // wider records, fewer dependent steps: the same 69 MiB table, 64 VALU per step
+        const size_t mib = 69;
+        for (int loads : {4, 6, 8}) {
+            const unsigned nrec = (unsigned)(mib * 1048576 / (16 * loads));
+            const int steps = loads == 4 ? 256 : (loads == 6 ? 171 : 128);  // equal bytes per lane
+            const double ms = loads == 4 ? run_l<4>(d, nrec, out, blocks, steps, 3)
+                                         : loads == 6 ? run_l<6>(d, nrec, out, blocks, steps, 3)
+                                                      : run_l<8>(d, nrec, out, blocks, steps, 3);
+            std::printf("{\"record_loads\": %d, \"steps\": %d, \"ms\": %.4f, \"g_req_per_s\": %.1f, \"g_steps_per_s\": %.1f}\n",
+                        loads, steps, ms, (double)blocks * 256 * steps * loads / ms / 1e6,
+                        (double)blocks * 256 * steps / ms / 1e6);
+        }
+        return 0;
+    }
     if (argc >= 4) {
         one((size_t)std::atoi(argv[1]), std::atoi(argv[2]), std::atoi(argv[3]), 1);
     } else {
