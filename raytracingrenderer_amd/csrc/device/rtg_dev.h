@@ -442,4 +442,32 @@ RTG_D bool tri_intersect48(const DevTri48& T, v3 o, v3 d, W want, float& t, floa
     return true;
 }
 
+// The same test on the record in memory: n and v0 (the first 32 B, two dwordx4) decide t, and the
+// last 16 B (v1.z, v2) are loaded as one aligned dwordx4 only when t is a candidate (left to
+// itself the compiler re-loaded part of the second dwordx4 and split the third one in two).
+template <class W>
+RTG_D bool tri_intersect48p(const DevTri48* P, v3 o, v3 d, W want, float& t, float& u, float& v) {
+    const float4 A = P->a, B = P->b;
+    const v3 n = mk(A.x, A.y, A.z);
+    const float denom = dot(n, d);
+    if (denom == 0) return false;
+    const v3 v0 = mk(A.w, B.x, B.y);
+    const float dd = dot(n, v0);
+    const float tt = (dd - dot(n, o)) / denom;
+    if (tt < 0 || !want(tt)) return false;
+    const float4 Cc = P->c;
+    const v3 v1 = mk(B.z, B.w, Cc.x), v2 = mk(Cc.y, Cc.z, Cc.w);
+    const v3 p = add(o, muls(d, tt));
+    const v3 e1 = sub(v2, v1), e2 = sub(v0, v2);
+    const float inv_area = 1.0f / dot(cross(e1, e2), n);
+    const float uu = dot(cross(e1, sub(p, v1)), n) * inv_area;
+    if (uu < 0 || uu > 1.0f) return false;
+    const float vv = dot(cross(e2, sub(p, v2)), n) * inv_area;
+    if (vv < 0 || (uu + vv) > 1.0f) return false;
+    t = tt;
+    u = uu;
+    v = vv;
+    return true;
+}
+
 }  // namespace rtgd

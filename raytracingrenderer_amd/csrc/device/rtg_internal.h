@@ -27,6 +27,9 @@ using namespace rtgd;
 #ifndef RTG_REFILL
 #define RTG_REFILL 12       // refill idle lanes once at least this many are idle (the setup code then
 #endif                      // runs with more lanes per execution)
+#ifndef RTG_TRI_SPLIT
+#define RTG_TRI_SPLIT 1     // triangle record: two dwordx4 for t, the third only for a candidate t
+#endif
 #ifndef RTG_TRACE_WPE
 #define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel
 #endif

@@ -165,7 +165,11 @@ void k_trace(SceneView s, TraceIO io) {
                 const int tri = start + k;
                 if (COUNT) (anyr ? c_stris : c_tris) += 1;
                 float t, u, v;
-#if RTG_TRI48
+#if RTG_TRI48 && RTG_TRI_SPLIT
+                const bool hit = tri_intersect48p(s.tris48 + tri, o, d, [&](float tt) {
+                    return anyr ? (tt < tbest && tt > RTG_EPS) : (tt <= tbest && tt > RTG_EPS);
+                }, t, u, v);
+#elif RTG_TRI48
                 const DevTri48 T = s.tris48[tri];
                 const bool hit = tri_intersect48(T, o, d, [&](float tt) {
                     return anyr ? (tt < tbest && tt > RTG_EPS) : (tt <= tbest && tt > RTG_EPS);
