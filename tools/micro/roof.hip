@@ -47,7 +47,7 @@ void k_chain(const float4* __restrict__ tab, unsigned nrec, int steps, float* ou
     out[gid] = acc;
 }
 
-template <int LOADS>
+template <int LOADS, int VALU = 64>
 static double run_l(const float4* d, unsigned nrec, float* out, int blocks, int steps, int reps) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
@@ -55,7 +55,7 @@ static double run_l(const float4* d, unsigned nrec, float* out, int blocks, int 
     float best = 1e30f;
     for (int rep = 0; rep < reps; ++rep) {
         (void)hipEventRecord(a);
-        hipLaunchKernelGGL((k_chain<64, LOADS>), dim3(blocks), dim3(256), 0, 0, d, nrec, steps, out);
+        hipLaunchKernelGGL((k_chain<VALU, LOADS>), dim3(blocks), dim3(256), 0, 0, d, nrec, steps, out);
         (void)hipEventRecord(b);
         (void)hipEventSynchronize(b);
         float ms = 0;
@@ -118,15 +118,28 @@ int main(int argc, char** argv) {
         std::fflush(stdout);
     };
     if (argc == 2 && std::string(argv[1]) == "width") {
-        // wider records, fewer dependent steps: the same 69 MiB table, 64 VALU per step
+        // records of 1-8 dwordx4 loads, equal bytes per lane: the same 69 MiB table, 64 VALU per step
         const size_t mib = 69;
-        for (int loads : {4, 6, 8}) {
+        for (int loads : {1, 2, 3, 4, 6, 8}) {
             const unsigned nrec = (unsigned)(mib * 1048576 / (16 * loads));
-            const int steps = loads == 4 ? 256 : (loads == 6 ? 171 : 128);  // equal bytes per lane
-            const double ms = loads == 4 ? run_l<4>(d, nrec, out, blocks, steps, 3)
-                                         : loads == 6 ? run_l<6>(d, nrec, out, blocks, steps, 3)
-                                                      : run_l<8>(d, nrec, out, blocks, steps, 3);
-            std::printf("{\"record_loads\": %d, \"steps\": %d, \"ms\": %.4f, \"g_req_per_s\": %.1f, \"g_steps_per_s\": %.1f}\n",
+            const int steps = 1024 / loads;  // equal bytes per lane
+            const double ms = loads == 1 ? run_l<1>(d, nrec, out, blocks, steps, 3)
+                            : loads == 2 ? run_l<2>(d, nrec, out, blocks, steps, 3)
+                            : loads == 3 ? run_l<3>(d, nrec, out, blocks, steps, 3)
+                            : loads == 4 ? run_l<4>(d, nrec, out, blocks, steps, 3)
+                            : loads == 6 ? run_l<6>(d, nrec, out, blocks, steps, 3)
+                                         : run_l<8>(d, nrec, out, blocks, steps, 3);
+            std::printf("{\"record_loads\": %d, \"valu_per_step\": 64, \"steps\": %d, \"ms\": %.4f, \"g_req_per_s\": %.1f, \"g_steps_per_s\": %.1f}\n",
+                        loads, steps, ms, (double)blocks * 256 * steps * loads / ms / 1e6,
+                        (double)blocks * 256 * steps / ms / 1e6);
+        }
+        for (int loads : {1, 2, 4}) {  // the same without VALU between the steps
+            const unsigned nrec = (unsigned)(mib * 1048576 / (16 * loads));
+            const int steps = 1024 / loads;
+            const double ms = loads == 1 ? run_l<1, 0>(d, nrec, out, blocks, steps, 3)
+                            : loads == 2 ? run_l<2, 0>(d, nrec, out, blocks, steps, 3)
+                                         : run_l<4, 0>(d, nrec, out, blocks, steps, 3);
+            std::printf("{\"record_loads\": %d, \"valu_per_step\": 0, \"steps\": %d, \"ms\": %.4f, \"g_req_per_s\": %.1f, \"g_steps_per_s\": %.1f}\n",
                         loads, steps, ms, (double)blocks * 256 * steps * loads / ms / 1e6,
                         (double)blocks * 256 * steps / ms / 1e6);
         }
