@@ -96,7 +96,7 @@ int main(int argc, char** argv) {
     const size_t nfl = maxmib * 1048576 / 4;
     float4* d = nullptr;
     float* out = nullptr;
-    if (hipMalloc(&d, nfl * 4) != hipSuccess || hipMalloc(&out, (size_t)blocks * 256 * 4) != hipSuccess) {
+    if (hipMalloc(&d, nfl * 4) != hipSuccess || hipMalloc(&out, (size_t)(dev_cus > 0 ? dev_cus : 256) * 16 * 256 * 4) != hipSuccess) {
         std::fprintf(stderr, "hipMalloc failed\n");
         return 1;
     }
@@ -142,6 +142,20 @@ int main(int argc, char** argv) {
             std::printf("{\"record_loads\": %d, \"valu_per_step\": 0, \"steps\": %d, \"ms\": %.4f, \"g_req_per_s\": %.1f, \"g_steps_per_s\": %.1f}\n",
                         loads, steps, ms, (double)blocks * 256 * steps * loads / ms / 1e6,
                         (double)blocks * 256 * steps / ms / 1e6);
+        }
+        return 0;
+    }
+    if (argc == 2 && std::string(argv[1]) == "occ") {
+        // chains in flight: blocks per CU = waves per SIMD (4 waves per block), 64-B records, 69 MiB
+        const size_t mib = 69;
+        const unsigned nrec = (unsigned)(mib * 1048576 / 64);
+        const int cus = dev_cus > 0 ? dev_cus : 256;
+        for (int wps : {1, 2, 3, 4, 6, 8, 12, 16}) {
+            const int nb = cus * wps;
+            const int steps = 256;
+            const double ms = run_l<4>(d, nrec, out, nb, steps, 3);
+            std::printf("{\"waves_per_simd\": %d, \"blocks\": %d, \"ms\": %.4f, \"g_steps_per_s\": %.1f}\n", wps, nb,
+                        ms, (double)nb * 256 * steps / ms / 1e6);
         }
         return 0;
     }
