@@ -226,16 +226,24 @@ def main():
     ms_step = t_max * 1e3 / a.steps
 
     # roofline for the dominant kernel, k_trace (one launch per bounce traces the extension rays of
-    # bounce b and the shadow rays of bounce b-1). Its limiter is the vector-memory request rate
-    # (TA busy ~87 %): every lane of a node step issues four 16-B loads of its own 64-B record at a
-    # data-dependent address (triangles: three). achieved = the walk's 16-B requests (counted on the
-    # same workload by the untimed counting pass) / the k_trace HIP-event time of the timed region;
-    # peak = the same request shape's ceiling measured by tools/micro/roof.hip (dependent random 64-B
-    # per-lane records from a 69 MiB table, the hot scene's size, at k_trace's occupancy).
+    # bounce b and the shadow rays of bounce b-1). Its limiter is the memory system's throughput of
+    # dependent random per-lane record fetches: a node step fetches its own 64-B record (four 16-B
+    # loads) at an address the previous step produced, a triangle test its 48-B record's first 32 B,
+    # a candidate hit its leaf box: each a line no lane of the wave needed a step earlier. (A
+    # triangle's last 16 B, fetched when its plane distance is a candidate, lie in the head's line
+    # in 6 of 8 records, and the per-ray queue / ray reads are coalesced: reported, not counted.) The
+    # ceiling microbenchmark (tools/micro/roof.hip: dependent random 64-B records, 69 MiB table = the
+    # hot scene, k_trace's occupancy) reaches ~162 G such fetches/s, flat from 2 to 16 waves per
+    # SIMD and only 13 % higher for 32-B records, so fetches, not bytes or 16-B
+    # requests, set the pace. achieved = the walk's fetches (counted on the same workload by the
+    # untimed counting pass) / the k_trace HIP-event time of the timed region. The 16-B request
+    # form of the same roofline is kept as a sub-object.
     n_steps = a.steps
-    req_step = (4.0 * cw["node_lane_steps"] + 3.0 * (cw["tri_tests"] + cw["shadow_tri_tests"])
-                + REQ_PER_RAY_IO * (cw["extension_rays"] + cw["shadow_rays"]))
-    req_totals = np.array([req_step * n_steps], dtype=np.float64)
+    all_rays = cw["extension_rays"] + cw["shadow_rays"]
+    rec_step = cw["node_lane_steps"] + cw["tri_tests"] + cw["shadow_tri_tests"] + cw["leafbox_tests"]
+    req_step = (4.0 * cw["node_lane_steps"] + 2.0 * (cw["tri_tests"] + cw["shadow_tri_tests"])
+                + cw["tri_tail_loads"] + 2.0 * cw["leafbox_tests"] + REQ_PER_RAY_IO * all_rays)
+    req_totals = np.array([req_step * n_steps, rec_step * n_steps], dtype=np.float64)
     # SURVEY.md §8d algorithmic bytes B = 32 B x box tests + 36 B x triangle tests + 48 B ray I/O,
     # with the box / triangle tests of the reference's own walk (BVH2, counted on the same workload);
     # these bytes are served by L1/L2/Infinity Cache, so they are compared with the L2 bandwidth
@@ -253,6 +261,7 @@ def main():
         dist.all_reduce(rt_, op=dist.ReduceOp.SUM)
         req_totals = rt_.cpu().numpy()
     achieved_req = req_totals[0] / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
+    achieved_rec = req_totals[1] / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
     ceiling = request_ceiling()
     avg_launch_s = extend_ms / max(extend_launches, 1) / 1e3
     # measured HBM traffic per launch (PMC, profiles/): only for the profiled workload (C3, 64 spp,
@@ -295,19 +304,28 @@ def main():
                            a.width, a.height, a.spp, a.max_depth),
                        "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
                        "max_depth": a.max_depth, "parallelism": "tile-sharded x%d + RCCL film reduce" % world},
-            "roofline": {"bound": "vmem-requests", "kernel": "k_trace (extension + shadow rays)",
-                         "achieved": None if achieved_req is None else round(achieved_req, 1),
-                         "peak": None if ceiling is None else round(ceiling["g_req_per_s"], 1),
-                         "unit": "G 16-B vector-memory requests/s",
-                         "frac": (round(achieved_req / ceiling["g_req_per_s"], 4)
-                                  if achieved_req and ceiling else None),
+            "roofline": {"bound": "dependent-random-record-fetches", "kernel": "k_trace (extension + shadow rays)",
+                         "achieved": None if achieved_rec is None else round(achieved_rec, 1),
+                         "peak": None if ceiling is None else round(ceiling["g_lane_steps_per_s"], 1),
+                         "unit": "G dependent random per-lane record fetches/s (node steps + triangle heads + leaf boxes)",
+                         "frac": (round(achieved_rec / ceiling["g_lane_steps_per_s"], 4)
+                                  if achieved_rec and ceiling else None),
                          "traffic": traffic,
                          "ceiling": (None if ceiling is None else
                                      "tools/micro/roof.hip, %s: dependent random 64-B per-lane records (4 x "
-                                     "dwordx4), %d MiB table, %d VALU/step, k_trace's occupancy"
+                                     "dwordx4), %d MiB table, %d VALU/step, k_trace's occupancy (flat from 2 to 16 "
+                                     "waves/SIMD: profiles/r02_roof_occ.jsonl)"
                                      % (os.path.relpath(ROOF_SWEEP, ROOT), ceiling["table_mib"],
                                         ceiling["valu_per_step"])),
-                         "requests_per_ray": round(req_step / max(cw["extension_rays"] + cw["shadow_rays"], 1), 2),
+                         "fetches_per_ray": round(rec_step / max(all_rays, 1), 2),
+                         "requests": {"achieved": None if achieved_req is None else round(achieved_req, 1),
+                                      "peak": None if ceiling is None else round(ceiling["g_req_per_s"], 1),
+                                      "unit": "G 16-B vector-memory requests/s",
+                                      "frac": (round(achieved_req / ceiling["g_req_per_s"], 4)
+                                               if achieved_req and ceiling else None),
+                                      "per_ray": round(req_step / max(all_rays, 1), 2)},
+                         "tri_tail_loads_per_ray": round(cw["tri_tail_loads"] / max(all_rays, 1), 2),
+                         "leafbox_tests_per_ray": round(cw["leafbox_tests"] / max(all_rays, 1), 2),
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                          "hbm": {"bytes_per_launch": traffic,
                                  "achieved_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic and extend_ms > 0 else None,

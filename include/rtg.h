@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 2
+#define RTG_ABI_VERSION 3
 
 /* error codes */
 #define RTG_OK              0
@@ -115,6 +115,9 @@ typedef struct rtg_stats {
     uint64_t leaf_phase_slots;     /* RTG_OPT_COUNT: leaf-phase iterations x 64 lanes           */
     uint64_t pops;                 /* RTG_OPT_COUNT: closest-hit stack pops                     */
     uint64_t cullable_pops;        /* RTG_OPT_COUNT: pops whose entry distance was > the hit    */
+    uint64_t tri_tail_loads;       /* RTG_OPT_COUNT: triangle records whose last 16 B were fetched */
+                                   /* (the plane distance was a candidate), all rays             */
+    uint64_t leafbox_tests;        /* RTG_OPT_COUNT: reference leaf-box records fetched, all rays */
 } rtg_stats;
 
 typedef struct rtg_handle rtg_handle;

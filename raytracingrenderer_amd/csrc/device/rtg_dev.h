@@ -446,7 +446,7 @@ RTG_D bool tri_intersect48(const DevTri48& T, v3 o, v3 d, W want, float& t, floa
 // last 16 B (v1.z, v2) are loaded as one aligned dwordx4 only when t is a candidate (left to
 // itself the compiler re-loaded part of the second dwordx4 and split the third one in two).
 template <class W>
-RTG_D bool tri_intersect48p(const DevTri48* P, v3 o, v3 d, W want, float& t, float& u, float& v) {
+RTG_D bool tri_intersect48p(const DevTri48* P, v3 o, v3 d, W want, float& t, float& u, float& v, unsigned& tails) {
     const float4 A = P->a, B = P->b;
     const v3 n = mk(A.x, A.y, A.z);
     const float denom = dot(n, d);
@@ -455,6 +455,7 @@ RTG_D bool tri_intersect48p(const DevTri48* P, v3 o, v3 d, W want, float& t, flo
     const float dd = dot(n, v0);
     const float tt = (dd - dot(n, o)) / denom;
     if (tt < 0 || !want(tt)) return false;
+    ++tails;  // (counting builds only: unused otherwise)
     const float4 Cc = P->c;
     const v3 v1 = mk(B.z, B.w, Cc.x), v2 = mk(Cc.y, Cc.z, Cc.w);
     const v3 p = add(o, muls(d, tt));

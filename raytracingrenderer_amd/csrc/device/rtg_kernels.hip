@@ -50,7 +50,8 @@ void k_trace(SceneView s, TraceIO io) {
     const unsigned nc = io.count ? *io.count : 0u;
     const unsigned n = nc + (io.scount ? *io.scount : 0u);
     unsigned long long c_nodes = 0, c_tris = 0, c_snodes = 0, c_stris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0,
-                       c_cullpop = 0, c_pops = 0, c_lslots = 0;
+                       c_cullpop = 0, c_pops = 0, c_lslots = 0, c_lbox = 0;
+    unsigned c_tails = 0;  // triangle records whose last 16 B were fetched (COUNT)
     unsigned pool_base = 0, pool_left = 0, last_b = 0;  // wave-uniform
     // batch size: RTG_FETCH, or (RTG_FETCH_ADAPT) about 1/16 of a wave's share of this launch
     const unsigned fetch_big = RTG_FETCH_ADAPT ? min((unsigned)RTG_FETCH, max(64u, n / (gthreads / 64u) / 16u))
@@ -168,7 +169,7 @@ void k_trace(SceneView s, TraceIO io) {
 #if RTG_TRI48 && RTG_TRI_SPLIT
                 const bool hit = tri_intersect48p(s.tris48 + tri, o, d, [&](float tt) {
                     return anyr ? (tt < tbest && tt > RTG_EPS) : (tt <= tbest && tt > RTG_EPS);
-                }, t, u, v);
+                }, t, u, v, c_tails);
 #elif RTG_TRI48
                 const DevTri48 T = s.tris48[tri];
                 const bool hit = tri_intersect48(T, o, d, [&](float tt) {
@@ -186,6 +187,7 @@ void k_trace(SceneView s, TraceIO io) {
                         // the exact box of the reference leaf holding this triangle (stored per
                         // triangle: a wide leaf slot may join sibling reference leaves)
                         const float4 b0 = s.leafbox[2 * tri], b1 = s.leafbox[2 * tri + 1];
+                        if (COUNT) c_lbox += 1;
                         cand = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
                     }
 #endif
@@ -456,6 +458,8 @@ void k_trace(SceneView s, TraceIO io) {
             c_lstep += __shfl_down(c_lstep, off);
             c_cullpop += __shfl_down(c_cullpop, off);
             c_pops += __shfl_down(c_pops, off);
+            c_lbox += __shfl_down(c_lbox, off);
+            c_tails += __shfl_down(c_tails, off);
         }
         if (lane == 0) {
             atomicAdd(&io.stats[0], c_nodes);
@@ -468,6 +472,8 @@ void k_trace(SceneView s, TraceIO io) {
             atomicAdd(&io.stats[13], c_lslots);
             atomicAdd(&io.stats[11], c_cullpop);
             atomicAdd(&io.stats[12], c_pops);
+            atomicAdd(&io.stats[6], (unsigned long long)c_tails);
+            atomicAdd(&io.stats[7], c_lbox);
         }
     }
 }
@@ -2358,6 +2364,8 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     h->stats.leaf_phase_slots = c[13];
     h->stats.cullable_pops = c[11];
     h->stats.pops = c[12];
+    h->stats.tri_tail_loads = c[6];
+    h->stats.leafbox_tests = c[7];
     *out = h->stats;
     return RTG_OK;
 }
