@@ -31,6 +31,7 @@
 extern "C" {
 #endif
 
+/* 2: rtg_scene_desc.projection; 3: rtg_stats.tri_tail_loads / leafbox_tests appended */
 #define RTG_ABI_VERSION 3
 
 /* error codes */
