@@ -28,18 +28,27 @@ L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, same guide (§L2)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
 ROOF_TABLE_MIB = 69  # the hot scene of C3: 21 MB wide nodes + 48 MB triangle records
+HOT_BYTES_PER_TRI = 69.0  # wide nodes (~21 B per triangle on C3) + the 48-B triangle record
 # per-ray queue id + ray origin + direction reads and the hit / visibility write (16-B requests)
 REQ_PER_RAY_IO = 4.0
 
 
-def request_ceiling():
-    """Best request rate of the ceiling microbenchmark on the table matching k_trace's hot scene."""
+def request_ceiling(n_tris=None):
+    """Best row of the ceiling microbenchmark on the table matching k_trace's hot scene: the
+    smallest swept table that holds the scene's wide nodes + triangle records (C3: 69 MiB)."""
     try:
         rows = [json.loads(l) for l in open(ROOF_SWEEP) if l.strip().startswith("{")]
     except OSError:
         return None
-    rows = [r for r in rows if r.get("table_mib") == ROOF_TABLE_MIB]
-    return max(rows, key=lambda r: r["g_req_per_s"]) if rows else None
+    sizes = sorted({r["table_mib"] for r in rows if "table_mib" in r})
+    if not sizes:
+        return None
+    mib = ROOF_TABLE_MIB
+    if n_tris is not None:
+        hot = n_tris * HOT_BYTES_PER_TRI / 1048576.0
+        mib = next((m for m in sizes if m >= hot), sizes[-1])
+    rows = [r for r in rows if r.get("table_mib") == mib]
+    return max(rows, key=lambda r: r["g_lane_steps_per_s"]) if rows else None
 # BASELINE.json configs (SURVEY.md §8): scene, size, spp, MAX_DEPTH. C1 is the CPU-only case.
 CONFIGS = {
     "C2": {"scene": "cornell-box", "width": 1024, "height": 1024, "spp": 64, "depth": 8},
@@ -262,7 +271,7 @@ def main():
         req_totals = rt_.cpu().numpy()
     achieved_req = req_totals[0] / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
     achieved_rec = req_totals[1] / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
-    ceiling = request_ceiling()
+    ceiling = request_ceiling(scene.desc.n_tris)
     avg_launch_s = extend_ms / max(extend_launches, 1) / 1e3
     # measured HBM traffic per launch (PMC, profiles/): only for the profiled workload (C3, 64 spp,
     # one rank); other configs, shards and N > 1 have other launch sizes and report null

@@ -8,7 +8,7 @@
 // dependent VALU ops per step, at k_trace's occupancy (256-thread blocks, 6 waves per SIMD, 1536
 // blocks on 256 CUs). It reports G 16-B requests/s = lanes x steps x 4 / time.
 //
-//   roof                      sweep: tables 21 / 69 / 1024 MiB x VALU 0 / 32 / 64 -> JSON lines
+//   roof                      sweep: tables 1 / 21 / 69 / 1024 MiB x VALU 0 / 32 / 64 -> JSON lines
 //   roof T V STEPS            one configuration (for rocprofv3 --pmc passes: FETCH_SIZE
 //                             calibration on a table larger than the 256 MiB Infinity Cache)
 // Build: hipcc --offload-arch=gfx950 -O3 -o roof roof.hip
@@ -162,7 +162,7 @@ int main(int argc, char** argv) {
     if (argc >= 4) {
         one((size_t)std::atoi(argv[1]), std::atoi(argv[2]), std::atoi(argv[3]), 1);
     } else {
-        for (size_t mib : {21, 69, 1024})
+        for (size_t mib : {1, 21, 69, 1024})
             for (int valu : {0, 32, 64}) one(mib, valu, 256, 3);
     }
     (void)hipFree(d);
