@@ -549,3 +549,21 @@ def test_full_size_configs_sampled_pixels(cfg):
     for smp in range(spp):  # Film::splat: film += L, sample by sample, in float32
         want = want + o.trace_paths(pix, np.full(npix, smp, np.uint32), seed=1234)
     assert_bitexact(film.reshape(-1, 3)[pix], want, "%s sampled pixels" % cfg)
+
+
+def test_count_mode_counters_are_consistent(synth20k, cornell256):
+    """RTG_OPT_COUNT (the bench's untimed counting pass): counting leaves the film unchanged, and
+    the walk counters nest (a leaf-box test needs a hit, a hit a fetched triangle tail, a tail a
+    triangle test), which the roofline's fetch counts rely on."""
+    for scene in (synth20k, cornell256):
+        rt = RayTracer(scene, seed=1234, max_depth=4)
+        rt.render(2, first_sample=0)
+        plain = rt.film()[0].copy()
+        rt.set_options(flags=N.RTG_OPT_CULL | N.RTG_OPT_COUNT)
+        rt.clear()
+        rt.render(2, first_sample=0)
+        s = rt.stats()
+        assert_bitexact(rt.film()[0], plain, "counting pass film")
+        tris = s["tri_tests"] + s["shadow_tri_tests"]
+        assert 0 < s["leafbox_tests"] <= s["tri_tail_loads"] <= tris, s
+        assert s["node_lane_steps"] > 0 and s["extension_rays"] > 0, s
