@@ -159,7 +159,9 @@ struct __align__(16) DevShade {
 };
 struct __align__(16) DevMat {
     int kind, two_sided, tex, is_light;
-    float int_ior, ext_ior, pad0, pad1;
+    float int_ior, ext_ior;
+    int tex_wh;  // the albedo texture's width | height << 16; `tex` is its first texel in SceneView::texels
+    int pad;
     float4 emission;
 };
 struct __align__(16) DevLight {
@@ -191,6 +193,7 @@ struct SceneView {
     const float4* texels;  // RGB + pad per texel
     int n_lights;
     int env_tex;         // -1: BackgroundColour(0)
+    int env_off, env_w, env_h;  // the environment texture (first texel, size), kernel-argument copies
     int root_word;       // child word of the root (RTG_EXIT if no triangles)
     int root_wordw;      // root word in the wide tree
     int usew;            // wide tree available (finite bounds, children inside parents)
@@ -230,9 +233,10 @@ RTG_D v3 bilinear(TX texel, int w, int h, float tu, float tv) {
     v3 s2 = texel(y1 * w + x), s3 = texel(y1 * w + x1);
     return add(add(add(muls(s0, w0), muls(s1, w1)), muls(s2, w2)), muls(s3, w3));
 }
-RTG_D v3 tex_sample(const SceneView& s, int tex, float tu, float tv) {
-    DevTex ti = s.texinfo[tex];
-    return bilinear(Texels4{s.texels + ti.off}, ti.w, ti.h, tu, tv);
+// A material carries its texture's offset and size, and the environment's are kernel arguments, so
+// the texels are one dependent fetch after the material record (no texinfo lookup between).
+RTG_D v3 tex_sample(const SceneView& s, const DevMat& M, float tu, float tv) {
+    return bilinear(Texels4{s.texels + M.tex}, M.tex_wh & 0xffff, (int)((unsigned)M.tex_wh >> 16), tu, tv);
 }
 
 // ------------------------------------------------------------------ sampling (Sampling.h)
@@ -260,7 +264,7 @@ RTG_D v3 env_eval(const SceneView& s, v3 wi) {
     u = (u < 0.0f) ? (float)((double)u + 2.0 * RTM_PI) : u;
     u = (float)((double)u / (2.0 * RTM_PI));
     float v = (float)((double)rtm_acosf(wi.y) / RTM_PI);
-    return tex_sample(s, s.env_tex, u, v);
+    return bilinear(Texels4{s.texels + s.env_off}, s.env_w, s.env_h, u, v);
 }
 RTG_D v3 background(const SceneView& s, v3 dir) {
     if (s.env_tex < 0) return mk(0.0f, 0.0f, 0.0f);  // BackgroundColour(0,0,0)::evaluate

@@ -805,7 +805,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                 const float t = h.x;
                 const v3 x = add(o, muls(d, t));  // Ray::at
                 const DevShade S = s.shade[tri];
-                const DevMat M = s.mats[__float_as_int(S.d.w)];
+                const DevMat& M = s.mats[__float_as_int(S.d.w)];
                 const v3 n0 = mk(S.a.x, S.a.y, S.a.z), n1 = mk(S.a.w, S.b.x, S.b.y), n2 = mk(S.b.z, S.b.w, S.c.x);
                 v3 sn = normalize(add(add(muls(n0, alpha), muls(n1, beta)), muls(n2, gamma)));
                 const float tu = (S.c.y * alpha + S.c.w * beta) + S.d.y * gamma;
@@ -819,7 +819,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                     c = (ALT && a.mode != RTG_INTEGRATOR_PATH) ? mk(M.emission.x, M.emission.y, M.emission.z)  // emit()
                         : can_hit ? mul(thr, mk(M.emission.x, M.emission.y, M.emission.z)) : mk(0.0f, 0.0f, 0.0f);
                 } else if (ALT && a.mode == RTG_INTEGRATOR_ALBEDO) {  // BSDF::evaluate(sd, (0,1,0))
-                    const v3 alb = tex_sample(s, M.tex, tu, tv);
+                    const v3 alb = tex_sample(s, M, tu, tv);
                     c = M.kind == RTG_MAT_MIRROR ? alb : (M.kind == RTG_MAT_GLASS ? mk(0.0f, 0.0f, 0.0f) : divs(alb, RTG_PI_F));
                 } else if (ALT && a.mode == RTG_INTEGRATOR_DIRECT_MIS) {
                     // computeDirectMIS, first half (Renderer.h:474-519): one light sample weighted by
@@ -831,7 +831,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                         int li = (int)((float)nl * pcg_next(st, inc));
                         li = (nl - 1) < li ? (nl - 1) : li;
                         const DevLight L = s.lights[li];
-                        const v3 f = divs(tex_sample(s, M.tex, tu, tv), RTG_PI_F);  // BSDF::evaluate
+                        const v3 f = divs(tex_sample(s, M, tu, tv), RTG_PI_F);  // BSDF::evaluate
                         float pdf;
                         float env_flag = 0.0f;
                         if (__float_as_int(L.v1t.w) == 0) {
@@ -888,7 +888,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                         v3 val;
                         float pdf_b;
                         PcgSampler smp{st, inc};
-                        const v3 wib = bsdf_sample(M.kind, M.int_ior, M.ext_ior, tex_sample(s, M.tex, tu, tv), fr, wo, smp,
+                        const v3 wib = bsdf_sample(M.kind, M.int_ior, M.ext_ior, tex_sample(s, M, tu, tv), fr, wo, smp,
                                                    val, pdf_b);
                         st = smp.s;
                         const v3 no = add(x, muls(wib, RTG_EPS));
@@ -903,7 +903,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                 } else {
                     const bool spec = M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS;
                     // albedo->sample(tu, tv): one fetch for BSDF::evaluate (NEE) and BSDF::sample
-                    const v3 alb = tex_sample(s, M.tex, tu, tv);
+                    const v3 alb = tex_sample(s, M, tu, tv);
                     // ---- computeDirect (Renderer.h:423-473)
                     v3 ld = mk(0.0f, 0.0f, 0.0f);
                     bool ld_pre = false;  // contrib takes the visible NEE value now (RTG_SHC_SPEC)
@@ -1776,6 +1776,13 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             texels.insert(texels.end(), {t.texels[3 * j], t.texels[3 * j + 1], t.texels[3 * j + 2], 0.0f});
     }
     if (d->env_texture >= (int)d->n_textures) { g_err = "env texture out of range"; return RTG_ERR_ARG; }
+    for (uint32_t i = 0; i < d->n_materials; ++i) {  // texture offset and size into the material record
+        const DevTex& t = texinfo[mats[i].tex];
+        if (t.w > 0xffff || t.h > 0xffff) { g_err = "texture larger than 65535 texels per side"; return RTG_ERR_ARG; }
+        mats[i].tex = t.off;
+        mats[i].tex_wh = t.w | (t.h << 16);
+        mats[i].pad = 0;
+    }
     std::vector<DevLight> lights(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; ++i) {
         int li = d->lights[i];
@@ -1822,6 +1829,9 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     s.texels = (const float4*)h->d_texels;
     s.n_lights = (int)d->n_lights;
     s.env_tex = d->env_texture;
+    s.env_off = d->env_texture >= 0 ? texinfo[d->env_texture].off : 0;
+    s.env_w = d->env_texture >= 0 ? texinfo[d->env_texture].w : 1;
+    s.env_h = d->env_texture >= 0 ? texinfo[d->env_texture].h : 1;
     s.root_word = root_word;
     s.nodesw = h->d_nodesw;
     s.nodesq = h->d_nodesq;

@@ -250,7 +250,7 @@ __global__ __launch_bounds__(RTG_TB) void k_light_shade(SceneView s, LightArgs a
                 if (M.is_light || spec) {
                     cont = false;  // lightTracePath returns at lights and pure specular surfaces
                 } else {
-                    const v3 f = divs(tex_sample(s, M.tex, tu, tv), RTG_PI_F);  // BSDF::evaluate
+                    const v3 f = divs(tex_sample(s, M, tu, tv), RTG_PI_F);  // BSDF::evaluate
                     const v3 col = mul(mul(thr, f), le);
                     int pixel;
                     v3 cc;
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(RTG_TB) void k_light_shade(SceneView s, LightArgs a
                 }
             } else if (!M.is_light && !spec) {
                 // store a VPL: Le = pathThroughput * Le * evaluate(sd, -r.dir) * |(-r.dir) . sN|
-                const v3 f = divs(tex_sample(s, M.tex, tu, tv), RTG_PI_F);
+                const v3 f = divs(tex_sample(s, M, tu, tv), RTG_PI_F);
                 const v3 vle = muls(mul(mul(thr, le), f), fabsf(dot(wo, sn)));
                 const unsigned r = atomicAdd(rec_n, 1u);
                 rec_key[r] = ((unsigned long long)i << 16) | k;
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(RTG_TB) void k_light_shade(SceneView s, LightArgs a
                     v3 ind;
                     float pdf;
                     PcgSampler smp{st, inc};
-                    const v3 wi = bsdf_sample(M.kind, M.int_ior, M.ext_ior, tex_sample(s, M.tex, tu, tv), fr, wo, smp,
+                    const v3 wi = bsdf_sample(M.kind, M.int_ior, M.ext_ior, tex_sample(s, M, tu, tv), fr, wo, smp,
                                               ind, pdf);
                     st = smp.s;
                     thr = divs(muls(mul(thr, ind), fabsf(dot(wi, sn))), pdf);
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(RTG_TB) void k_ir_first_hit(SceneView s, ChunkArgs 
         if (M.two_sided && dot(neg(d), sn) < 0) sn = neg(sn);
         const bool spec = M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS;
         flag = (M.is_light || spec) ? 1.0f : 2.0f;
-        if (!M.is_light && !spec) f = divs(tex_sample(s, M.tex, tu, tv), RTG_PI_F);
+        if (!M.is_light && !spec) f = divs(tex_sample(s, M, tu, tv), RTG_PI_F);
     }
     px[lp] = make_float4(x.x, x.y, x.z, flag);
     pn[lp] = make_float4(sn.x, sn.y, sn.z, 0.0f);
