@@ -163,6 +163,7 @@ struct __align__(16) DevMat {
     int tex_wh;  // the albedo texture's width | height << 16; `tex` is its first texel in SceneView::texels
     int pad;
     float4 emission;
+    float4 texel0;  // a 1x1 texture's texel (RGB): bilinear() then needs no fetch
 };
 struct __align__(16) DevLight {
     float4 v0a;  // v0.xyz, area       (area light)
@@ -212,7 +213,7 @@ struct Texels4 {
     RTG_D v3 operator()(int i) const { const float4 v = t[i]; return mk(v.x, v.y, v.z); }
 };
 template <class TX>
-RTG_D v3 bilinear(TX texel, int w, int h, float tu, float tv) {
+RTG_D v3 bilinear(TX texel, int w, int h, float tu, float tv, const float4* one = nullptr) {
     float au = fabsf(tu), av = fabsf(tv);
     float u = smax(0.0f, au) * (float)w;
     float v = smax(0.0f, av) * (float)h;
@@ -226,17 +227,25 @@ RTG_D v3 bilinear(TX texel, int w, int h, float tu, float tv) {
     float w3 = fu * fv;
     // x, y >= 0 here (u, v are >= 0 or +inf), so the modulo runs only when the coordinate wraps
     // and (x + 1) % w is a compare: same values as the reference's x % w, (x + 1) % w
-    x = x < w ? x : x % w;
-    y = y < h ? y : y % h;
-    const int x1 = (x + 1 == w) ? 0 : x + 1, y1 = (y + 1 == h) ? 0 : y + 1;
-    v3 s0 = texel(y * w + x), s1 = texel(y * w + x1);
-    v3 s2 = texel(y1 * w + x), s3 = texel(y1 * w + x1);
+    v3 s0, s1, s2, s3;
+    if (one) {  // 1x1 texture: every index wraps to texel 0, whose value the caller holds
+        s0 = s1 = s2 = s3 = mk(one->x, one->y, one->z);
+    } else {
+        x = x < w ? x : x % w;
+        y = y < h ? y : y % h;
+        const int x1 = (x + 1 == w) ? 0 : x + 1, y1 = (y + 1 == h) ? 0 : y + 1;
+        s0 = texel(y * w + x);
+        s1 = texel(y * w + x1);
+        s2 = texel(y1 * w + x);
+        s3 = texel(y1 * w + x1);
+    }
     return add(add(add(muls(s0, w0), muls(s1, w1)), muls(s2, w2)), muls(s3, w3));
 }
 // A material carries its texture's offset and size, and the environment's are kernel arguments, so
 // the texels are one dependent fetch after the material record (no texinfo lookup between).
 RTG_D v3 tex_sample(const SceneView& s, const DevMat& M, float tu, float tv) {
-    return bilinear(Texels4{s.texels + M.tex}, M.tex_wh & 0xffff, (int)((unsigned)M.tex_wh >> 16), tu, tv);
+    return bilinear(Texels4{s.texels + M.tex}, M.tex_wh & 0xffff, (int)((unsigned)M.tex_wh >> 16), tu, tv,
+                    M.tex_wh == 0x10001 ? &M.texel0 : nullptr);
 }
 
 // ------------------------------------------------------------------ sampling (Sampling.h)

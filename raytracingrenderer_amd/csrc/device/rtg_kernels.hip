@@ -1782,6 +1782,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         mats[i].tex = t.off;
         mats[i].tex_wh = t.w | (t.h << 16);
         mats[i].pad = 0;
+        mats[i].texel0 = make_float4(texels[(size_t)t.off * 4], texels[(size_t)t.off * 4 + 1], texels[(size_t)t.off * 4 + 2], 0.0f);
     }
     std::vector<DevLight> lights(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; ++i) {
