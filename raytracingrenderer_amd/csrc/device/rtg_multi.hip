@@ -61,6 +61,15 @@ bool load_rccl() {
     if (!g_rccl.ok) g_err = "RCCL: missing symbols";
     return g_rccl.ok;
 }
+
+// the reduce's two timing events on device 0, destroyed on every return path
+struct EventPair {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    ~EventPair() {
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+    }
+};
 }  // namespace
 
 struct rtg_group {
@@ -200,25 +209,29 @@ int rtg_group_reduce(rtg_group* g) {
     if (!g) return RTG_ERR_ARG;
     const size_t n = g->h.size();
     const size_t count = (size_t)g->W * g->H * 3;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    EventPair ev;
     HIPOK(hipSetDevice(g->devices[0]));
-    HIPOK(hipEventCreate(&e0));
-    HIPOK(hipEventCreate(&e1));
-    HIPOK(hipEventRecord(e0, g->h[0]->stream));
+    HIPOK(hipEventCreate(&ev.e0));
+    HIPOK(hipEventCreate(&ev.e1));
+    HIPOK(hipEventRecord(ev.e0, g->h[0]->stream));
     if (!g->comms.empty()) {
-        // every rank's film (summed in sample order on its device) -> device 0, ncclSum
+        // every rank's film (summed in sample order on its device) -> device 0, ncclSum. Every
+        // failure inside the group still closes it (ncclGroupEnd), so the thread's RCCL group
+        // state stays balanced.
         if (g_rccl.group_start() != ncclSuccess) { g_err = "ncclGroupStart failed"; return RTG_ERR_HIP; }
-        for (size_t r = 0; r < n; ++r) {
-            HIPOK(hipSetDevice(g->devices[r]));
+        std::string fail;
+        for (size_t r = 0; r < n && fail.empty(); ++r) {
+            const hipError_t he = hipSetDevice(g->devices[r]);
+            if (he != hipSuccess) {
+                fail = std::string("hipSetDevice: ") + hipGetErrorString(he);
+                break;
+            }
             const ncclResult_t nr = g_rccl.reduce(g->h[r]->d_film, r == 0 ? g->d_sum : nullptr, count, ncclFloat, ncclSum,
                                                   0, g->comms[r], g->h[r]->stream);
-            if (nr != ncclSuccess) {
-                (void)g_rccl.group_end();
-                g_err = std::string("ncclReduce: ") + g_rccl.error_string(nr);
-                return RTG_ERR_HIP;
-            }
+            if (nr != ncclSuccess) fail = std::string("ncclReduce: ") + g_rccl.error_string(nr);
         }
         const ncclResult_t nr = g_rccl.group_end();
+        if (!fail.empty()) { g_err = fail; return RTG_ERR_HIP; }
         if (nr != ncclSuccess) { g_err = std::string("ncclGroupEnd: ") + g_rccl.error_string(nr); return RTG_ERR_HIP; }
         for (size_t r = 0; r < n; ++r) {
             HIPOK(hipSetDevice(g->devices[r]));
@@ -237,13 +250,11 @@ int rtg_group_reduce(rtg_group* g) {
         HIPOK(hipMemcpy(g->d_sum, sum.data(), count * sizeof(float), hipMemcpyHostToDevice));
     }
     HIPOK(hipSetDevice(g->devices[0]));
-    HIPOK(hipEventRecord(e1, g->h[0]->stream));
-    HIPOK(hipEventSynchronize(e1));
+    HIPOK(hipEventRecord(ev.e1, g->h[0]->stream));
+    HIPOK(hipEventSynchronize(ev.e1));
     float ms = 0.0f;
-    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventElapsedTime(&ms, ev.e0, ev.e1);
     g->reduce_ms = ms;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     g->reduced_spp = g->h[0]->spp;
     g->reduced = true;
     return RTG_OK;
