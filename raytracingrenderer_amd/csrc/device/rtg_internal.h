@@ -234,6 +234,7 @@ struct rtg_handle {
     PathBufs pb[2]{};
     hipStream_t stream2 = nullptr;
     int pipes = 1, stagger = 2;
+    int shade_grid = 1;  // RTG_SHADE_GRID: k > 0: P / (256 k) blocks of k tiles each; 0: persistent (n_cu x occupancy)
     hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};  // fork, stagger, join, accumulate-order
     unsigned* d_pix = nullptr;
     size_t cap_pix = 0;

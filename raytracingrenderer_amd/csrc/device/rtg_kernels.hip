@@ -1879,6 +1879,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     int occs = 0;
     HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occs, k_shade<false>, RTG_TB, 0));
     h->shade_blocks = h->n_cu * std::max(1, occs);
+    if (const char* e = std::getenv("RTG_SHADE_GRID")) h->shade_grid = std::atoi(e);
     return ensure_ovf(h);
 }
 
@@ -2094,10 +2095,12 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         for (int b = 0; b <= maxb; ++b) {
             if (b > 0) {
                 timed_begin(h, cs, k);
+                const unsigned sgrid = h->shade_grid > 0 ? (unsigned)((a.P + (size_t)RTG_TB * h->shade_grid - 1) / ((size_t)RTG_TB * h->shade_grid))
+                                                         : (unsigned)h->shade_blocks;
                 if (h->integrator == RTG_INTEGRATOR_PATH)
-                    hipLaunchKernelGGL(k_shade<false>, dim3(h->shade_blocks), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
+                    hipLaunchKernelGGL(k_shade<false>, dim3(sgrid), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
                 else
-                    hipLaunchKernelGGL(k_shade<true>, dim3(h->shade_blocks), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
+                    hipLaunchKernelGGL(k_shade<true>, dim3(sgrid), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
                 LAUNCH_OK("k_shade");
                 timed_end(h, cs, k); kinds.push_back(2); ++k;
             }
