@@ -27,6 +27,9 @@ using namespace rtgd;
 #ifndef RTG_REFILL
 #define RTG_REFILL 12       // refill idle lanes once at least this many are idle (the setup code then
 #endif                      // runs with more lanes per execution)
+#ifndef RTG_SLICE_MIX
+#define RTG_SLICE_MIX 1     // 1: each of the 8 work slices = an eighth of the extension rays, then an
+#endif                      //    eighth of the shadow rays (k_trace)
 #ifndef RTG_TRI_SPLIT
 #define RTG_TRI_SPLIT 1     // triangle record: two dwordx4 for t, the third only for a candidate t
 #endif

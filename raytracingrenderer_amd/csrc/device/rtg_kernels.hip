@@ -57,7 +57,15 @@ void k_trace(SceneView s, TraceIO io) {
     const unsigned fetch_big = RTG_FETCH_ADAPT ? min((unsigned)RTG_FETCH, max(64u, n / (gthreads / 64u) / 16u))
                                                : (unsigned)RTG_FETCH;
     const unsigned tail_rays = (gthreads / 64u) * fetch_big * RTG_FETCH_TAIL / (io.fetch8 ? 8u : 1u);
-    auto slice_lo = [&](int k) { return io.fetch8 ? (unsigned)(((unsigned long long)n * (unsigned)k) >> 3) : 0u; };
+    const unsigned ns = n - nc;
+    // RTG_SLICE_MIX: slice k holds the k-th eighth of the extension rays followed by the k-th eighth
+    // of the shadow rays (every XCD walks long closest-hit rays first and ends on any-hit rays);
+    // otherwise slice k is the k-th eighth of the combined index space [extension | shadow]
+    auto slice_lo = [&](int k) {
+        return !io.fetch8 ? 0u
+               : RTG_SLICE_MIX ? (unsigned)(((unsigned long long)nc * (unsigned)k) >> 3) + (unsigned)(((unsigned long long)ns * (unsigned)k) >> 3)
+                               : (unsigned)(((unsigned long long)n * (unsigned)k) >> 3);
+    };
     int slice = io.fetch8 ? (int)(blockIdx.x & 7u) : 0, tried = 0;  // wave-uniform
     unsigned s_lo = slice_lo(slice), s_len = (io.fetch8 ? slice_lo(slice + 1) : n) - s_lo;
     bool drained = false;                   // wave-uniform
@@ -115,6 +123,12 @@ void k_trace(SceneView s, TraceIO io) {
                 const unsigned take = min((unsigned)__popcll(im), pool_left);
                 if (!have && pos < take) {
                     ri = pool_base + pos;
+                    if (RTG_SLICE_MIX && io.fetch8) {
+                        const unsigned e_lo = (unsigned)(((unsigned long long)nc * (unsigned)slice) >> 3);
+                        const unsigned e_len = (unsigned)(((unsigned long long)nc * (unsigned)(slice + 1)) >> 3) - e_lo;
+                        const unsigned j = ri - s_lo;
+                        ri = j < e_len ? e_lo + j : nc + (unsigned)(((unsigned long long)ns * (unsigned)slice) >> 3) + (j - e_len);
+                    }
                     have = true;
                     anyr = ri >= nc;
                     pid = (int)(anyr ? io.squeue[ri - nc] : (io.queue ? io.queue[ri] : ri));
