@@ -244,6 +244,16 @@ int  rtg_trace_closest(rtg_handle* h, const float* rays, uint32_t n, float* hits
  * out: n*11 floats (wi.xyz, reflectedColour.rgb, pdf, draws consumed, evaluate(wi).rgb). */
 int  rtg_probe_bsdf(const float* cases, uint32_t n, float* out);
 int  rtg_trace_visible(rtg_handle* h, const float* rays, uint32_t n, int32_t* visible);
+/* Transcendental probe on the current device: the kernels' acosf / sinf / cosf / atan2f
+ * (include/rtg_math.h, the reference platform's glibc restated; RTBase/Sampling.h:35-61,
+ * Core.h:549-557, Lights.h:152-155) on n inputs. fn: RTG_MATH_SINF, _COSF, _SINCOSF (out 2n:
+ * sin, cos), _ACOSF, _ATAN2F (in 2n: y, x). n < 2^31. */
+#define RTG_MATH_SINF   0
+#define RTG_MATH_COSF   1
+#define RTG_MATH_SINCOSF 2
+#define RTG_MATH_ACOSF  3
+#define RTG_MATH_ATAN2F 4
+int  rtg_probe_math(int fn, const float* in, uint32_t n, float* out);
 
 #ifdef __cplusplus
 }

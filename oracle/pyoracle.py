@@ -46,6 +46,8 @@ def lib(flavour="rtm"):
             getattr(L, fn).argtypes = [C.c_float]
         L.or_atan2f.restype = C.c_float
         L.or_atan2f.argtypes = [C.c_float, C.c_float]
+        L.or_math_eval.restype = None
+        L.or_math_eval.argtypes = [C.c_int, f32p, C.c_uint32, f32p]
         L.or_sincos_mismatch.restype = C.c_long
         L.or_sincos_mismatch.argtypes = [f32p, C.c_long]
         _libs[flavour] = L

@@ -1168,6 +1168,24 @@ float or_acosf(float x) { return O_ACOSF(x); }
 float or_sinf(float x) { return O_SINF(x); }
 float or_cosf(float x) { return O_COSF(x); }
 float or_atan2f(float y, float x) { return O_ATAN2F(y, x); }
+/* The flavour's transcendentals on arrays (fn as rtg_probe_math: 0 sinf, 1 cosf, 2 sincosf -> 2n
+ * outputs, 3 acosf, 4 atan2f <- 2n inputs y, x): the libm build calls the C library. */
+void or_math_eval(int fn, const float* in, uint32_t n, float* out)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        switch (fn) {
+        case 0: out[i] = O_SINF(in[i]); break;
+        case 1: out[i] = O_COSF(in[i]); break;
+#if ORACLE_LIBM
+        case 2: sincosf(in[i], &out[2 * (size_t)i], &out[2 * (size_t)i + 1]); break;
+#else
+        case 2: rtm_sincosf(in[i], &out[2 * (size_t)i], &out[2 * (size_t)i + 1]); break;
+#endif
+        case 3: out[i] = O_ACOSF(in[i]); break;
+        default: out[i] = O_ATAN2F(in[2 * (size_t)i], in[2 * (size_t)i + 1]); break;
+        }
+    }
+}
 /* rtm_sincosf (the GPU's fused form) against rtm_sinf / rtm_cosf on n inputs: number of inputs
  * whose bits differ in either result. */
 long or_sincos_mismatch(const float* x, long n)

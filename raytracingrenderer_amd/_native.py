@@ -93,6 +93,7 @@ RTG_EXPORTS = [
     ("rtg_trace_closest", C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),
     ("rtg_trace_visible", C.c_int, [C.c_void_p, f32p, C.c_uint32, i32p]),
     ("rtg_probe_bsdf", C.c_int, [f32p, C.c_uint32, f32p]),
+    ("rtg_probe_math", C.c_int, [C.c_int, f32p, C.c_uint32, f32p]),
     # one node, several GPUs (rtg_multi.hip): tile stripes per device + one RCCL film reduce
     ("rtg_tiles_for_rank", C.c_int, [C.c_uint32, C.c_uint32, C.c_int, C.c_int, u32p, u32p]),
     ("rtg_group_create", C.c_int, [i32p, C.c_int, C.POINTER(rtg_scene_desc), C.POINTER(C.c_void_p)]),

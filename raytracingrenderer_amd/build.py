@@ -6,6 +6,7 @@ Outputs (git-ignored, shipped to the GPU box with the source snapshot):
   raytracingrenderer_amd/lib/rtg_render      headless CLI (-scene -SPP -outputFilename)
   oracle/_build/liboracle_rtm.so             test-only CPU restatement, shared math
   oracle/_build/liboracle_libm.so            test-only CPU restatement, C-library math
+  oracle/_build/libm_check                   test-only: include/rtg_math.h vs the host glibc
 Every float-producing unit is compiled with -ffp-contract=off (bit-faithful arithmetic).
 """
 import os
@@ -91,6 +92,11 @@ def build_oracle(force=False):
             _run(["gcc", "-std=c11", "-O2", "-ffp-contract=off", "-fPIC", "-shared", "-D_GNU_SOURCE",
                   "-DORACLE_LIBM=" + libm, "-o", out, src, "-lm", "-lpthread"])
         outs.append(out)
+    chk = os.path.join(ORACLE_BUILD, "libm_check")
+    chk_src = os.path.join(ORACLE, "libm_check.c")
+    if force or _newer(chk, _deps([chk_src])):
+        _run(["gcc", "-std=c11", "-O2", "-ffp-contract=off", "-fno-builtin", "-pthread", "-o", chk, chk_src, "-lm"])
+    outs.append(chk)
     return outs
 
 

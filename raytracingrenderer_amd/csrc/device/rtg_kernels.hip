@@ -1169,6 +1169,20 @@ __global__ void k_probe_bsdf(const float* in, int n, float* out) {
     o[8] = ev.x; o[9] = ev.y; o[10] = ev.z;
 }
 
+// Transcendental probe: the device's include/rtg_math.h on given inputs (parity vs the host glibc).
+// fn 0 sinf, 1 cosf, 2 sincosf (out: sin, cos per input), 3 acosf, 4 atan2f (in: y, x per input).
+__global__ void k_probe_math(int fn, const float* in, int n, float* out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    switch (fn) {
+    case 0: out[i] = rtm_sinf(in[i]); break;
+    case 1: out[i] = rtm_cosf(in[i]); break;
+    case 2: rtm_sincosf(in[i], &out[2 * (size_t)i], &out[2 * (size_t)i + 1]); break;
+    case 3: out[i] = rtm_acosf(in[i]); break;
+    default: out[i] = rtm_atan2f(in[2 * (size_t)i], in[2 * (size_t)i + 1]); break;
+    }
+}
+
 // Per-chunk ray tally: extension + shadow queue lengths of every bounce into stats[2..3].
 __global__ void k_tally(const Counters* ctr, int maxb, unsigned long long* stats) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -2469,6 +2483,23 @@ int rtg_probe_bsdf(const float* cases, uint32_t n, float* out) {
     HIPOK(hipGetLastError());
     HIPOK(hipDeviceSynchronize());
     HIPOK(hipMemcpy(out, d_out, (size_t)n * 11 * sizeof(float), hipMemcpyDeviceToHost));
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return RTG_OK;
+}
+
+int rtg_probe_math(int fn, const float* in, uint32_t n, float* out) {
+    if (!in || !out || fn < 0 || fn > 4 || n > 0x7fffffffu) return RTG_ERR_ARG;
+    if (n == 0) return RTG_OK;
+    const size_t nin = (size_t)n * (fn == 4 ? 2 : 1), nout = (size_t)n * (fn == 2 ? 2 : 1);
+    float *d_in = nullptr, *d_out = nullptr;
+    HIPOK(hipMalloc((void**)&d_in, nin * sizeof(float)));
+    HIPOK(hipMalloc((void**)&d_out, nout * sizeof(float)));
+    HIPOK(hipMemcpy(d_in, in, nin * sizeof(float), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_probe_math, dim3((n + 255) / 256), dim3(256), 0, nullptr, fn, d_in, (int)n, d_out);
+    HIPOK(hipGetLastError());
+    HIPOK(hipDeviceSynchronize());
+    HIPOK(hipMemcpy(out, d_out, nout * sizeof(float), hipMemcpyDeviceToHost));
     (void)hipFree(d_in);
     (void)hipFree(d_out);
     return RTG_OK;

@@ -1,6 +1,7 @@
 """GPU parity: the HIP wavefront renderer (librtg.so, called through the C-ABI) against the C oracle
 with the same transcendentals (bit-exact), the reference's own traversal / BSDF code (golden
 fixtures from oracle/_ref), and size-independent properties at full BASELINE sizes."""
+import ctypes as C
 import hashlib
 import json
 import os
@@ -473,12 +474,14 @@ def test_adaptive_render_many_frames_and_key_limit():
     assert_bitexact(after, before, "film untouched by a rejected adaptive call")
 
 
+@pytest.mark.parametrize("flavour", ["rtm", "libm"])
 @pytest.mark.parametrize("case", ["cornell-mat", "bathroom", "coffee+GI", "synth20k"])
-def test_gpu_film_vs_reference_classes(case, synth20k):
+def test_gpu_film_vs_reference_classes(case, flavour, synth20k):
     """The GPU film against RayTracer::pathTrace restated on RTBase's own compiled classes
-    (oracle/_ref libref_rtm.so: the reference's BVH traversal, shading, BSDFs, lights, camera and
-    Film, with the shared transcendentals interposed), bit for bit: a film-level pin that does not
-    go through the C oracle."""
+    (oracle/_ref: the reference's BVH traversal, shading, BSDFs, lights, camera and Film), bit for
+    bit: a film-level pin that does not go through the C oracle. libref.so calls the C library's
+    transcendentals (the reference as built on Linux); libref_rtm.so has include/rtg_math.h's
+    interposed (the same bits, which is what this shows at the film level)."""
     from oracle import pyref
     if not pyref.available():
         pytest.fail("oracle/_ref (libref_rtm.so) missing: build it where /root/reference exists")
@@ -494,10 +497,44 @@ def test_gpu_film_vs_reference_classes(case, synth20k):
             "coffee+GI": (staged("coffee"), dict(width=80, height=100, skip_missing=True, envmap="GI.hdr"), 4, 3, 5),
         }[case]
         path = name
-    r = pyref.RefScene(path, kw["width"], kw["height"], kw.get("skip_missing", False), kw.get("envmap"), flavour="rtm")
+    r = pyref.RefScene(path, kw["width"], kw["height"], kw.get("skip_missing", False), kw.get("envmap"),
+                       flavour=flavour)
     ref, _ = r.render(spp, seed=seed, max_depth=depth, threads=8)
     s = loadScene(path, **kw)
-    assert_bitexact(gpu_film(s, spp, seed=seed, max_depth=depth), ref, "GPU vs reference classes (%s)" % case)
+    assert_bitexact(gpu_film(s, spp, seed=seed, max_depth=depth), ref,
+                    "GPU vs reference classes (%s, %s)" % (case, flavour))
+
+
+def _nan_canon(a):
+    return np.where(np.isnan(a), np.float32(np.nan), a).view(np.uint32)
+
+
+def test_device_math_matches_glibc():
+    """The kernels' transcendentals (include/rtg_math.h compiled for gfx950, rtg_probe_math) against
+    the host C library (liboracle_libm's or_math_eval calls glibc), bit for bit (any NaN equals any
+    NaN): every 97th float bit pattern (44M inputs over all exponents) for sinf / cosf / sincosf /
+    acosf, and 8M (y, x) pairs for atan2f (random bit patterns and unit-vector components)."""
+    from oracle.pyoracle import lib
+    G = lib("libm")
+    x = np.arange(0, 1 << 32, 97, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    for fn, nout in ((0, len(x)), (1, len(x)), (2, 2 * len(x)), (3, len(x))):
+        got = np.zeros(nout, np.float32)
+        want = np.zeros(nout, np.float32)
+        assert N.rtg().rtg_probe_math(fn, N.ptr(x, C.c_float), len(x), N.ptr(got, C.c_float)) == 0
+        G.or_math_eval(fn, N.ptr(x, C.c_float), len(x), N.ptr(want, C.c_float))
+        bad = np.flatnonzero(_nan_canon(got) != _nan_canon(want))
+        assert bad.size == 0, (fn, bad.size, x[bad[:4] % len(x)].view(np.uint32), got[bad[:4]], want[bad[:4]])
+    rng = np.random.default_rng(5)
+    n = 1 << 23
+    yx = rng.integers(0, 1 << 32, size=2 * n, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    d = rng.normal(size=(n // 2, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    yx[: n] = d[:, [2, 0]].astype(np.float32).reshape(-1)  # EnvironmentMap::evaluate: atan2f(wi.z, wi.x)
+    got = np.zeros(n, np.float32)
+    want = np.zeros(n, np.float32)
+    assert N.rtg().rtg_probe_math(4, N.ptr(yx, C.c_float), n, N.ptr(got, C.c_float)) == 0
+    G.or_math_eval(4, N.ptr(yx, C.c_float), n, N.ptr(want, C.c_float))
+    assert np.array_equal(_nan_canon(got), _nan_canon(want))
 
 
 @pytest.mark.parametrize("scene_name", ["cornell-box", "cornell-mat"])

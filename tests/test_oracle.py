@@ -39,7 +39,9 @@ def test_c1_known_answer_glibc(cornell256):
 
 
 def test_c1_shared_math_known_answer(cornell256):
+    """With include/rtg_math.h (the GPU's transcendentals) the oracle gives the survey's glibc md5."""
     film, _ = Oracle(cornell256, 4, "rtm").render(4, seed=1234, threads=8)
+    assert FILM_KAT["C1_rtm"]["md5"] == FILM_KAT["C1_libm"]["md5"]
     assert md5(film / np.float32(4.0)) == FILM_KAT["C1_rtm"]["md5"]
 
 
