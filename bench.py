@@ -354,7 +354,7 @@ def main():
                                          "bytes_per_shadow_ray": round(b_sray, 1),
                                          "shadow_box_tests_per_ray": round(s_boxes_per_ray, 2),
                                          "shadow_tri_tests_per_ray": round(s_tris_per_ray, 2)},
-                         "walk": "bvh2" if a.bvh2 else ("bvh4 (collapsed from the reference BVH2)" if os.environ.get("RTG_REBUILD") == "0" else "bvh4 (collapsed from an own 3-axis SAH tree over the reference leaves)"),
+                         "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from an own 3-axis SAH tree over the reference leaves)",
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
                          "node_steps_per_ray": round(cw["node_lane_steps"] / max(cw["extension_rays"] + cw["shadow_rays"], 1), 2),

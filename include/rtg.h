@@ -143,6 +143,7 @@ void rtg_destroy(rtg_handle* h);
 #define RTG_OPT_COUNT  2
 #define RTG_OPT_TIMING 4
 #define RTG_OPT_BVH2   8
+#define RTG_OPT_WAVETIME 16  /* diagnostic builds only (RTG_DEBUG=1): per-wave clocks of k_trace on stderr */
 int  rtg_set_options(rtg_handle* h, int max_depth, int flags, uint32_t max_paths_in_flight);
 
 /* Per-pixel estimator (the alternative RayTracer methods of Renderer.h). PATH is RayTracer::render's

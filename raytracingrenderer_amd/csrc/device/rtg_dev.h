@@ -15,13 +15,6 @@
 #include <stdint.h>
 
 #include "../../../include/rtg_math.h"
-#ifdef RTG_TIMING_ONLY_FAST_MATH  // A/B experiment only: NOT bit-faithful, never shipped
-#define rtm_sinf(x) __sinf(x)
-#define rtm_cosf(x) __cosf(x)
-#define rtm_sincosf(x, s, c) __sincosf(x, s, c)
-#define rtm_acosf(x) acosf(x)
-#define rtm_atan2f(y, x) atan2f(y, x)
-#endif
 
 #define RTG_D __device__ __forceinline__
 #define RTG_FLT_MAX 3.40282347e+38f
@@ -85,17 +78,6 @@ struct __align__(16) DevNode {
     float4 c;  // rmin.z rmax.x rmax.y rmax.z
     int4 d;    // left word, right word, -, -
 };
-// Wide node collapsed from the reference BVH2: its slots are a cut of the BVH2 subtree (leaves stay
-// slots). RTG_WIDTH*32 bytes: six planes of RTG_WIDTH floats (min x,y,z, max x,y,z; slot k's box in
-// element k), RTG_WIDTH child words (RTG_EXIT = empty slot), RTG_WIDTH pad words.
-#ifndef RTG_WIDTH
-#define RTG_WIDTH 4
-#endif
-#define RTG_WQ (RTG_WIDTH / 4)         // float4s per plane
-#define RTG_WNODE_F4 (RTG_WIDTH * 2)   // float4s per node
-struct __align__(16) DevNodeW {
-    float4 q[RTG_WNODE_F4];
-};
 // Compressed 4-wide node (64 B). Slot boxes are stored conservatively: 8-bit offsets from the
 // node's min corner in power-of-two steps, rounded outward and checked on the host with the
 // device's own decode arithmetic, so a decoded box always contains the exact one. Exactness then
@@ -105,50 +87,21 @@ struct __align__(16) DevNodeW {
 //   q[1] = planes min x, min y, min z, max x  (byte k = slot k)
 //   q[2] = planes max y, max z, child words 0, 1
 //   q[3] = child words 2, 3, -, -
-#ifndef RTG_QNODE
-#define RTG_QNODE 1
-#endif
-// RTG_NODE48: the same node in 48 B (three dwordx4 loads). The origin keeps a 16-bit mantissa
-// (rounded down) and its low byte carries the axis exponent; the child words are 24-bit
-// (bit 23: leaf, 0xffffff: empty):
-//   q[0] = origin.x|exp.x, origin.y|exp.y, origin.z|exp.z, plane min x
-//   q[1] = planes min y, min z, max x, max y;   q[2] = plane max z, words (4 x 24 bits)
-#ifndef RTG_NODE48
-#define RTG_NODE48 0
-#endif
+// (A 48-B form and a 32-B form with 4-bit planes were measured slower: DESIGN.md §4.)
 struct __align__(16) DevNodeQ {
-    float4 q[RTG_NODE48 ? 3 : 4];
+    float4 q[4];
 };
-RTG_D int word24(unsigned w) {
-    return w == 0xffffffu ? RTG_EXIT : ((w & 0x800000u) ? ~(int)(w & 0x7fffffu) : (int)w);
-}
 typedef float f2 __attribute__((ext_vector_type(2)));  // packed FP32 pair (v_pk_fma/mul/add_f32)
 __host__ __device__ inline float qdecode(float origin, unsigned plane, int k, float scale) {
     return origin + (float)((plane >> (8 * k)) & 255u) * scale;
 }
-// Hot intersection record (64 B): exactly the operands of Triangle::rayIntersect.
-struct __align__(16) DevTri {
-    float4 nd;    // n.xyz, d
-    float4 v1i;   // vertices[1].p, invArea = 1/Dot(e1 x e2, n)
-    float4 v2;    // vertices[2].p, -
-    float4 e2;    // e2 = v0 - v2, -   (e1 = v2 - v1 is recomputed: same float op)
-};
 // Compact intersection record (48 B, three dwordx4 loads): n and the three vertices. d, e1, e2
 // and invArea are recomputed with Triangle::init's own float ops (Geometry.h:72-83), so they are
-// the same bits as the 64-B record's stored values.
-#ifndef RTG_TRI48
-#define RTG_TRI48 1
-#endif
-#ifndef RTG_TRI_PAD
-#define RTG_TRI_PAD 0       // 1: 64-B stride (records never straddle a cache line), still 3 loads
-#endif
+// the same bits as a record that stores them.
 struct __align__(16) DevTri48 {
     float4 a;  // n.xyz, v0.x
     float4 b;  // v0.yz, v1.xy
     float4 c;  // v1.z, v2.xyz
-#if RTG_TRI_PAD
-    float4 pad;
-#endif
 };
 // Cold shading record (64 B): vertex normals, uvs, material.
 struct __align__(16) DevShade {
@@ -181,12 +134,10 @@ struct DevCamera {
 };
 
 struct SceneView {
-    const DevNode* nodes;
-    const DevNodeW* nodesw;  // collapsed wide tree (exact for rays with finite nonzero 1/d)
-    const DevNodeQ* nodesq;  // compressed 4-wide tree (RTG_QNODE)
+    const DevNode* nodes;    // reference BVH2 (rays with a zero direction component)
+    const DevNodeQ* nodesq;  // compressed 4-wide tree (exact for rays with finite nonzero 1/d)
     const float4* leafbox;   // [2 per triangle] exact box of the reference leaf holding it
-    const DevTri* tris;
-    const DevTri48* tris48;  // same triangles, compact record (RTG_TRI48)
+    const DevTri48* tris48;  // triangles (Triangle::rayIntersect's operands)
     const DevShade* shade;
     const DevMat* mats;
     const DevLight* lights;
@@ -408,53 +359,9 @@ RTG_D float slab_cull_entry(float mnx, float mny, float mnz, float mxx, float mx
     return fmaxf(fmaxf(cx, cy), cz);  // fmaxf drops NaN -> conservative
 }
 
-// Triangle::rayIntersect; t,u,v written only on success.
-RTG_D bool tri_intersect(const DevTri& T, v3 o, v3 d, float& t, float& u, float& v) {
-    v3 n = mk(T.nd.x, T.nd.y, T.nd.z);
-    float denom = dot(n, d);
-    if (denom == 0) return false;
-    float tt = (T.nd.w - dot(n, o)) / denom;
-    if (tt < 0) return false;
-    v3 p = add(o, muls(d, tt));
-    v3 v1 = mk(T.v1i.x, T.v1i.y, T.v1i.z), v2 = mk(T.v2.x, T.v2.y, T.v2.z);
-    v3 e1 = sub(v2, v1), e2 = mk(T.e2.x, T.e2.y, T.e2.z);
-    float inv_area = T.v1i.w;
-    float uu = dot(cross(e1, sub(p, v1)), n) * inv_area;
-    if (uu < 0 || uu > 1.0f) return false;
-    float vv = dot(cross(e2, sub(p, v2)), n) * inv_area;
-    if (vv < 0 || (uu + vv) > 1.0f) return false;
-    t = tt;
-    u = uu;
-    v = vv;
-    return true;
-}
-
-// Triangle::rayIntersect on the 48-B record. `want(t)` rejects a plane distance that cannot be a
-// candidate for the caller (beyond the current hit or not in front): those never produce output,
-// so the rest of the test (edge functions, 1/area) is skipped for them.
-template <typename W>
-RTG_D bool tri_intersect48(const DevTri48& T, v3 o, v3 d, W want, float& t, float& u, float& v) {
-    const v3 n = mk(T.a.x, T.a.y, T.a.z);
-    const float denom = dot(n, d);
-    if (denom == 0) return false;
-    const v3 v0 = mk(T.a.w, T.b.x, T.b.y);
-    const float dd = dot(n, v0);
-    const float tt = (dd - dot(n, o)) / denom;
-    if (tt < 0 || !want(tt)) return false;
-    const v3 v1 = mk(T.b.z, T.b.w, T.c.x), v2 = mk(T.c.y, T.c.z, T.c.w);
-    const v3 p = add(o, muls(d, tt));
-    const v3 e1 = sub(v2, v1), e2 = sub(v0, v2);
-    const float inv_area = 1.0f / dot(cross(e1, e2), n);
-    const float uu = dot(cross(e1, sub(p, v1)), n) * inv_area;
-    if (uu < 0 || uu > 1.0f) return false;
-    const float vv = dot(cross(e2, sub(p, v2)), n) * inv_area;
-    if (vv < 0 || (uu + vv) > 1.0f) return false;
-    t = tt;
-    u = uu;
-    v = vv;
-    return true;
-}
-
+// Triangle::rayIntersect on the 48-B record (Geometry.h:89-105). `want(t)` rejects a plane
+// distance that cannot be a candidate for the caller (beyond the current hit or not in front):
+// those never produce output, so the rest of the test (edge functions, 1/area) is skipped for them.
 // The same test on the record in memory: n and v0 (the first 32 B, two dwordx4) decide t, and the
 // last 16 B (v1.z, v2) are loaded as one aligned dwordx4 only when t is a candidate (left to
 // itself the compiler re-loaded part of the second dwordx4 and split the third one in two).

@@ -15,89 +15,28 @@ using namespace rtgd;
 
 #define RTG_TB 256          // threads per block (4 waves)
 #define RTG_POP ((int)0x80000001)  // "pop the stack" marker inside one traversal step
-#ifndef RTG_STACK
+// Measured constants of the traversal and shading kernels (DESIGN.md §4 records the A/B runs;
+// the rejected alternatives are archived under tools/experiments/, not compiled in):
 #define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (24 KB per block)
-#endif
-#ifndef RTG_POSTPONE
-#define RTG_POSTPONE 32     // >0: park a reached leaf and keep walking; run the leaves of a wave together
-#endif                      //     once this many lanes hold one (or no lane can walk on)
-#ifndef RTG_DRAIN_LEAF
-#define RTG_DRAIN_LEAF 1    // once the queue is empty, run the leaf phase whenever a lane has parked a
-#endif                      //     leaf (the drain is latency-bound: lanes should not wait for each other)
-#ifndef RTG_REFILL
+#define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
+                            // once this many lanes hold one (or no lane can walk on, or the queue is dry)
 #define RTG_REFILL 12       // refill idle lanes once at least this many are idle (the setup code then
-#endif                      // runs with more lanes per execution)
-#ifndef RTG_SLICE_MIX
-#define RTG_SLICE_MIX 1     // 1: each of the 8 work slices = an eighth of the extension rays, then an
-#endif                      //    eighth of the shadow rays (k_trace)
-#ifndef RTG_TRI_SPLIT
-#define RTG_TRI_SPLIT 1     // triangle record: two dwordx4 for t, the third only for a candidate t
-#endif
-#ifndef RTG_TRACE_WPE
-#define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel
-#endif
+                            // runs with more lanes per execution)
+#define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel (80 VGPRs)
 #define RTG_CULL_REL 1.52587890625e-05f  // 2^-16 relative inflation for distance culling
-#ifndef RTG_FETCH
-#define RTG_FETCH 256       // rays a wave takes from the work counter per atomic (k_trace pool; 64: -3.5 %)
-#endif
-#ifndef RTG_FETCH_TAIL
-#define RTG_FETCH_TAIL 8    // k: fetch 64 rays per atomic once about k rounds of big batches are left
-#endif
-#ifndef RTG_TAIL_BATCH
-#define RTG_TAIL_BATCH 64   // rays per atomic in the tail rounds
-#endif
-#ifndef RTG_WAVETIME
-#define RTG_WAVETIME 0      // 1: compile k_trace's per-wave clocks (diagnostic; RTG_WAVETIME env then enables)
-#endif
-#ifndef RTG_COLLAPSE_DP
-#define RTG_COLLAPSE_DP 0   // 1: SAH-optimal BVH2 -> 4-wide cut with leaf merging (env RTG_COLLAPSE=dp|greedy)
-#endif
-#ifndef RTG_GEN_LEAN
-#define RTG_GEN_LEAN 1      // bounce-0 path state implied instead of written by k_generate (ChunkArgs::lean)
-#endif
-#ifndef RTG_SHC_SPEC
-#define RTG_SHC_SPEC 1      // k_shade stores the NEE value in contrib up front; k_trace clears it on occlusion
-#endif
-#ifndef RTG_SHADE_PF
-#define RTG_SHADE_PF 0      // 1: k_shade loads the next iteration's path id one iteration ahead
-#endif
-#ifndef RTG_REBUILD
-#define RTG_REBUILD 1       // wide nodes cut from an own 3-axis SAH tree over the reference leaves (env RTG_REBUILD=0: from the reference BVH2)
-#endif
-#ifndef RTG_FETCH8
-#define RTG_FETCH8 1        // k_trace fetches from 8 slice counters (TraceIO::fetch8): +4 % per GPU at N=8
-#endif
-#ifndef RTG_FETCH_ADAPT
-#define RTG_FETCH_ADAPT 0   // 1: big batch = min(RTG_FETCH, ~1/16 of a wave's share) (no gain)
-#endif
-#ifndef RTG_SHADE_BUF
-#define RTG_SHADE_BUF 0     // >0: k_shade stages compacted path ids in LDS (entries per queue) and
-                            // appends them with one atomic per flush instead of one per 256 paths
-#endif
-#ifndef RTG_FAST_PUSH
-#define RTG_FAST_PUSH 1     // wide-node pushes as three unconditional LDS writes when they fit (~1 %)
-#endif
-#ifndef RTG_SEL_SORT
-#define RTG_SEL_SORT 0      // 1: slot sort network as selects instead of branches
-#endif
-#ifndef RTG_SHADE_SORT
-#define RTG_SHADE_SORT 0    // 1: k_shade partitions each block's paths into misses and hits first (C3: no change)
-#endif
-#ifndef RTG_SHADE_WAVES
-#define RTG_SHADE_WAVES 5                // min waves per SIMD for k_shade (96 VGPRs, no spills)
+#define RTG_FETCH 256       // rays a wave takes from a work counter per atomic (k_trace pool)
+#define RTG_FETCH_TAIL 8    // fetch RTG_TAIL_BATCH rays per atomic once about this many rounds of
+#define RTG_TAIL_BATCH 64   // big batches are left in the slice (shorter drain tails)
+#define RTG_SHADE_WAVES 5   // min waves per SIMD for k_shade (96 VGPRs, no spills)
+// RTG_DEBUG=1 (a diagnostic build only) compiles k_trace's per-wave clocks (RTG_OPT_WAVETIME).
+#ifndef RTG_DEBUG
+#define RTG_DEBUG 0
 #endif
 
-// Work counters of one bounce. Every field sits in its own 128-B line (RTG_CTR_PAD): the
-// device-scope atomics on them (queue appends in k_shade, work fetches in k_trace) are served one
-// line at a time, so counters sharing a line serialise with each other.
-#ifndef RTG_CTR_PAD
-#define RTG_CTR_PAD 1
-#endif
-#if RTG_CTR_PAD
+// Work counters of one bounce. Every field sits in its own 128-B line: the device-scope atomics on
+// them (queue appends in k_shade, work fetches in k_trace) are served one line at a time, so
+// counters sharing a line serialise with each other.
 #define RTG_CPAD(f) unsigned f; unsigned f##_pad[31];
-#else
-#define RTG_CPAD(f) unsigned f;
-#endif
 struct __align__(16) Counters {
     RTG_CPAD(n_ext) RTG_CPAD(n_shadow) RTG_CPAD(f_ext) RTG_CPAD(f_shadow) RTG_CPAD(f_shade) RTG_CPAD(pad0)
     RTG_CPAD(pad1) RTG_CPAD(pad2)
@@ -128,7 +67,7 @@ struct TraceIO {
     unsigned long long* stats; // [0,1] closest / [4,5] any-hit: box tests, triangle tests (COUNT)
     int cull;
     int wide;                  // traverse the 4-wide tree when the ray allows it
-    unsigned long long* wtime; // diagnostics (RTG_WAVETIME): per wave start / drained / exit clock
+    unsigned long long* wtime; // RTG_DEBUG builds: per wave start / drained / exit clock
     float4 cam_o;              // closest: the origin of every ray when ray_o is null (camera rays);
                                // a null queue is the identity (path id = ray index)
 };
@@ -139,10 +78,10 @@ struct ChunkArgs {
     unsigned long long seed;
     int max_depth;
     int mode;                  // RTG_INTEGRATOR_* (first-hit estimators never continue a path)
-    int pm;                    // path id order: 1 pixel-major (pid = lp * ns + sl), 0 sample-major
     DevCamera cam;
     int lean = 0;              // 1: bounce-0 state implied (identity queue, camera origin, thr 1,
                                // PCG seed, canHitLight); k_generate writes ray_d only
+    // path ids are pixel-major: pid = lp * ns + sl (a wave of camera rays is one pixel's samples)
 };
 
 struct PathBufs {
@@ -206,23 +145,19 @@ struct rtg_handle {
     uint32_t spp = 0;
     int max_depth = 4, cull = 1, count = 0, timing = 0;
     uint32_t max_paths = 1u << 30;  // 1G paths in flight at most; the chunk is held to half the free HBM
-    int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0, shade_blocks = 0, packet_blocks = 0;
-    int fetch8 = RTG_FETCH8;  // sliced work counters for k_trace (RTG_FETCH8 env overrides)
-    int pixel_major = 1;  // path ids pixel-major: a wave's rays share pixels (RTG_PIXEL_MAJOR=0: sample-major)
-    int packet = 0;  // RTG_PACKET=1: camera rays by the packet walk (exact, but slower: DESIGN.md §4)
+    int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0;
+    int wavetime = 0;  // RTG_DEBUG builds: per-wave clocks of the first chunk (RTG_OPT_WAVETIME)
     uint32_t bvh_depth = 0;
     SceneView sv{};
     DevCamera cam{};
     rtg_camera_proj proj{};  // projectOntoCamera state (light tracing, rtg_light.hip)
     DevNode* d_nodes = nullptr;
-    DevNodeW* d_nodesw = nullptr;
     DevNodeQ* d_nodesq = nullptr;
     float4* d_leafbox = nullptr;
     int usew = 0, wide = 1;
     int integrator = RTG_INTEGRATOR_PATH;
-    bool rebuilt = false;     // wide tree cut from rebuild_over_leaves (RTG_REBUILD)
+    bool rebuilt = false;     // wide tree cut from rebuild_over_leaves (else from the reference BVH2)
     uint32_t wide_depth = 0;  // wide levels on the longest root-to-leaf path
-    DevTri* d_tris = nullptr;
     DevTri48* d_tris48 = nullptr;
     DevShade* d_shade = nullptr;
     DevMat* d_mats = nullptr;
@@ -230,15 +165,10 @@ struct rtg_handle {
     DevTex* d_texinfo = nullptr;
     float* d_texels = nullptr;
     float* d_film = nullptr;
-    // chunk buffers
-    // two chunk pipelines (buffers, stream, overflow region each): pipeline 1 runs on stream2
-    size_t cap_P[2] = {0, 0};
-    int cap_maxb[2] = {0, 0};
-    PathBufs pb[2]{};
-    hipStream_t stream2 = nullptr;
-    int pipes = 1, stagger = 2;
-    int shade_grid = 1;  // RTG_SHADE_GRID: k > 0: P / (256 k) blocks of k tiles each; 0: persistent (n_cu x occupancy)
-    hipEvent_t pev[4] = {nullptr, nullptr, nullptr, nullptr};  // fork, stagger, join, accumulate-order
+    // chunk buffers (path state of the paths in flight)
+    size_t cap_P = 0;
+    int cap_maxb = 0;
+    PathBufs pb{};
     unsigned* d_pix = nullptr;
     size_t cap_pix = 0;
     std::vector<uint32_t> pix_key;
@@ -256,7 +186,7 @@ struct rtg_handle {
 // rtg_kernels.hip
 int ensure_ovf(rtg_handle* h);
 int set_pixels(rtg_handle* h, const uint32_t* tiles, uint32_t n_tiles);
-int ensure_chunk(rtg_handle* h, int i, size_t P, int maxb);
+int ensure_chunk(rtg_handle* h, size_t P, int maxb);
 int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed, const uint32_t* tiles,
                 uint32_t n_tiles, hipStream_t st);
 // k_generate for the paths of a (camera rays at pixel centres, Scene.h:43-54)

@@ -53,18 +53,14 @@ void k_trace(SceneView s, TraceIO io) {
                        c_cullpop = 0, c_pops = 0, c_lslots = 0, c_lbox = 0;
     unsigned c_tails = 0;  // triangle records whose last 16 B were fetched (COUNT)
     unsigned pool_base = 0, pool_left = 0, last_b = 0;  // wave-uniform
-    // batch size: RTG_FETCH, or (RTG_FETCH_ADAPT) about 1/16 of a wave's share of this launch
-    const unsigned fetch_big = RTG_FETCH_ADAPT ? min((unsigned)RTG_FETCH, max(64u, n / (gthreads / 64u) / 16u))
-                                               : (unsigned)RTG_FETCH;
-    const unsigned tail_rays = (gthreads / 64u) * fetch_big * RTG_FETCH_TAIL / (io.fetch8 ? 8u : 1u);
+    const unsigned tail_rays = (gthreads / 64u) * (unsigned)RTG_FETCH * RTG_FETCH_TAIL / (io.fetch8 ? 8u : 1u);
     const unsigned ns = n - nc;
-    // RTG_SLICE_MIX: slice k holds the k-th eighth of the extension rays followed by the k-th eighth
-    // of the shadow rays (every XCD walks long closest-hit rays first and ends on any-hit rays);
-    // otherwise slice k is the k-th eighth of the combined index space [extension | shadow]
+    // io.fetch8: 8 work slices (one counter each, by blockIdx % 8: one per XCD). Slice k holds the
+    // k-th eighth of the extension rays followed by the k-th eighth of the shadow rays, so every XCD
+    // walks long closest-hit rays first and ends on any-hit rays.
     auto slice_lo = [&](int k) {
         return !io.fetch8 ? 0u
-               : RTG_SLICE_MIX ? (unsigned)(((unsigned long long)nc * (unsigned)k) >> 3) + (unsigned)(((unsigned long long)ns * (unsigned)k) >> 3)
-                               : (unsigned)(((unsigned long long)n * (unsigned)k) >> 3);
+                          : (unsigned)(((unsigned long long)nc * (unsigned)k) >> 3) + (unsigned)(((unsigned long long)ns * (unsigned)k) >> 3);
     };
     int slice = io.fetch8 ? (int)(blockIdx.x & 7u) : 0, tried = 0;  // wave-uniform
     unsigned s_lo = slice_lo(slice), s_len = (io.fetch8 ? slice_lo(slice + 1) : n) - s_lo;
@@ -76,7 +72,7 @@ void k_trace(SceneView s, TraceIO io) {
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0, pend = RTG_EXIT;
     bool occluded = false, wide = false, anyr = false;  // anyr: this lane's ray is a shadow ray
     const unsigned wslot = gtid >> 6;
-    if (RTG_WAVETIME && io.wtime && lane == 0) io.wtime[3 * wslot] = __builtin_amdgcn_s_memrealtime();
+    if (RTG_DEBUG && io.wtime && lane == 0) io.wtime[3 * wslot] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         // ---- retire finished rays
         if (have && cur == RTG_EXIT && pend == RTG_EXIT) {
@@ -98,8 +94,8 @@ void k_trace(SceneView s, TraceIO io) {
             // slices with a counter each (the atomics of one counter serialise); a wave starts on
             // slice blockIdx % 8 and moves on to the next slice when its own runs dry.
             while (pool_left == 0) {
-                const bool tail = RTG_FETCH_TAIL && last_b + tail_rays >= s_len;
-                const unsigned g = tail ? (unsigned)RTG_TAIL_BATCH : fetch_big;
+                const bool tail = last_b + tail_rays >= s_len;
+                const unsigned g = tail ? (unsigned)RTG_TAIL_BATCH : (unsigned)RTG_FETCH;
                 unsigned b = 0;
                 if (lane == 0) b = atomicAdd(io.fetch8 ? io.fetch8 + 32 * slice : io.fetch, g);
                 b = __builtin_amdgcn_readfirstlane(b);  // wave-uniform: keeps the fetch state in SGPRs
@@ -109,7 +105,7 @@ void k_trace(SceneView s, TraceIO io) {
                     pool_left = min(g, s_len - b);
                 } else if (!io.fetch8 || ++tried == 8) {
                     drained = true;
-                    if (RTG_WAVETIME && io.wtime && lane == 0) io.wtime[3 * wslot + 1] = __builtin_amdgcn_s_memrealtime();
+                    if (RTG_DEBUG && io.wtime && lane == 0) io.wtime[3 * wslot + 1] = __builtin_amdgcn_s_memrealtime();
                     break;
                 } else {
                     slice = (slice + 1) & 7;
@@ -123,7 +119,7 @@ void k_trace(SceneView s, TraceIO io) {
                 const unsigned take = min((unsigned)__popcll(im), pool_left);
                 if (!have && pos < take) {
                     ri = pool_base + pos;
-                    if (RTG_SLICE_MIX && io.fetch8) {
+                    if (io.fetch8) {
                         const unsigned e_lo = (unsigned)(((unsigned long long)nc * (unsigned)slice) >> 3);
                         const unsigned e_len = (unsigned)(((unsigned long long)nc * (unsigned)(slice + 1)) >> 3) - e_lo;
                         const unsigned j = ri - s_lo;
@@ -144,7 +140,7 @@ void k_trace(SceneView s, TraceIO io) {
                     omag = s.cull_scale + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
                     dmag = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
                     delta = RTG_CULL_REL * (omag + (tbest < RTG_FLT_MAX ? tbest * dmag : 0.0f));
-                    bid = (RTG_SHC_SPEC && anyr && !io.visible && rd.w == 0.0f) ? -2 : -1;
+                    bid = (anyr && !io.visible && rd.w == 0.0f) ? -2 : -1;
                     bu = bv = 0.0f;
                     occluded = false;
                     sp = 0;
@@ -167,7 +163,6 @@ void k_trace(SceneView s, TraceIO io) {
         if (COUNT) {
             c_slots += 64;
             c_nstep += (have && cur >= 0) ? 1 : 0;
-            if (!RTG_POSTPONE) c_lstep += (have && cur != RTG_EXIT && cur < 0) ? 1 : 0;
         }
         if (!have || (cur == RTG_EXIT && pend == RTG_EXIT)) continue;
         // Leaf: the reference's leaf loop (Geometry.h:420-431 / 446-458) over 1-2 triangles (a wide
@@ -180,23 +175,12 @@ void k_trace(SceneView s, TraceIO io) {
                 const int tri = start + k;
                 if (COUNT) (anyr ? c_stris : c_tris) += 1;
                 float t, u, v;
-#if RTG_TRI48 && RTG_TRI_SPLIT
                 const bool hit = tri_intersect48p(s.tris48 + tri, o, d, [&](float tt) {
                     return anyr ? (tt < tbest && tt > RTG_EPS) : (tt <= tbest && tt > RTG_EPS);
                 }, t, u, v, c_tails);
-#elif RTG_TRI48
-                const DevTri48 T = s.tris48[tri];
-                const bool hit = tri_intersect48(T, o, d, [&](float tt) {
-                    return anyr ? (tt < tbest && tt > RTG_EPS) : (tt <= tbest && tt > RTG_EPS);
-                }, t, u, v);
-#else
-                const DevTri T = s.tris[tri];
-                const bool hit = tri_intersect(T, o, d, t, u, v);
-#endif
                 if (hit) {
                     bool cand = anyr ? !(t >= tbest || t <= RTG_EPS)
                                      : (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid)));
-#if RTG_QNODE
                     if (cand && wide) {
                         // the exact box of the reference leaf holding this triangle (stored per
                         // triangle: a wide leaf slot may join sibling reference leaves)
@@ -204,7 +188,6 @@ void k_trace(SceneView s, TraceIO io) {
                         if (COUNT) c_lbox += 1;
                         cand = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
                     }
-#endif
                     if (!cand) {
                     } else if (anyr) {
                         occluded = true;
@@ -220,27 +203,10 @@ void k_trace(SceneView s, TraceIO io) {
         };
         // ---- one traversal step
         if (cur >= 0 && wide) {
-            int wd[RTG_WIDTH];
-            float key[RTG_WIDTH];
-#if RTG_QNODE
+            int wd[4];
+            float key[4];
             {
                 const float4* np = s.nodesq[cur].q;
-#if RTG_NODE48
-                const float4 g0 = np[0], g1 = np[1], g2 = np[2];
-                const unsigned bx = __float_as_uint(g0.x), by = __float_as_uint(g0.y), bz = __float_as_uint(g0.z);
-                const float4 h0 = make_float4(__uint_as_float(bx & ~255u), __uint_as_float(by & ~255u),
-                                              __uint_as_float(bz & ~255u), 0.0f);
-                const float sx = __uint_as_float((bx & 255u) << 23);
-                const float sy = __uint_as_float((by & 255u) << 23);
-                const float sz = __uint_as_float((bz & 255u) << 23);
-                const unsigned p0 = __float_as_uint(g0.w), p1 = __float_as_uint(g1.x), p2 = __float_as_uint(g1.y);
-                const unsigned p3 = __float_as_uint(g1.z), p4 = __float_as_uint(g1.w), p5 = __float_as_uint(g2.x);
-                const unsigned w01 = __float_as_uint(g2.y), w12 = __float_as_uint(g2.z), w23 = __float_as_uint(g2.w);
-                wd[0] = word24(w01 & 0xffffffu);
-                wd[1] = word24((w01 >> 24) | ((w12 & 0xffffu) << 8));
-                wd[2] = word24((w12 >> 16) | ((w23 & 0xffu) << 16));
-                wd[3] = word24(w23 >> 8);
-#else
                 const float4 h0 = np[0], h1 = np[1], h2 = np[2], h3 = np[3];
                 const unsigned ex = __float_as_uint(h0.w);
                 const float sx = __uint_as_float((ex & 255u) << 23);
@@ -252,7 +218,6 @@ void k_trace(SceneView s, TraceIO io) {
                 wd[1] = __float_as_int(h2.w);
                 wd[2] = __float_as_int(h3.x);
                 wd[3] = __float_as_int(h3.y);
-#endif
                 // Conservative slot test in ray-relative form. Exactness does not need the exact slab
                 // test here: a candidate hit is accepted only after its reference leaf box passes the
                 // exact test, so a slot test only has to pass whenever the exact test on a reference
@@ -305,68 +270,17 @@ void k_trace(SceneView s, TraceIO io) {
                     }
                 }
             }
-#else
-            float pl[6][RTG_WIDTH];
-            const float4* np = s.nodesw[cur].q;
-#pragma unroll
-            for (int q = 0; q < 6 * RTG_WQ; ++q) {
-                const float4 v = np[q];
-                pl[q / RTG_WQ][(q % RTG_WQ) * 4 + 0] = v.x;
-                pl[q / RTG_WQ][(q % RTG_WQ) * 4 + 1] = v.y;
-                pl[q / RTG_WQ][(q % RTG_WQ) * 4 + 2] = v.z;
-                pl[q / RTG_WQ][(q % RTG_WQ) * 4 + 3] = v.w;
-            }
-#pragma unroll
-            for (int q = 0; q < RTG_WQ; ++q) {
-                const float4 v = np[6 * RTG_WQ + q];
-                wd[q * 4 + 0] = __float_as_int(v.x);
-                wd[q * 4 + 1] = __float_as_int(v.y);
-                wd[q * 4 + 2] = __float_as_int(v.z);
-                wd[q * 4 + 3] = __float_as_int(v.w);
-            }
-#pragma unroll
-            for (int k = 0; k < RTG_WIDTH; ++k) {
-                const float mnx = pl[0][k], mny = pl[1][k], mnz = pl[2][k];
-                const float mxx = pl[3][k], mxy = pl[4][k], mxz = pl[5][k];
-                bool hit = wd[k] != RTG_EXIT && slab_exact(mnx, mny, mnz, mxx, mxy, mxz, o, inv);
-                const float e = slab_cull_entry(mnx, mny, mnz, mxx, mxy, mxz, o, inv, delta);
-                if (io.cull) hit = hit && !(e > tbest);
-                if (COUNT) (anyr ? c_snodes : c_nodes) += wd[k] != RTG_EXIT ? 1 : 0;
-                key[k] = hit ? fmaxf(e, -RTG_FLT_MAX) : __builtin_inff();
-            }
-#endif
             // ascending entry distance (misses sort last); order only affects culling, not results
-#if RTG_SEL_SORT  // compare-exchange as selects (v_cndmask), no exec-mask branches
-#define RTG_CSWAP(i, j)                                                          \
-    {                                                                           \
-        const bool sw = key[j] < key[i];                                        \
-        const float ki = key[i], kj = key[j];                                   \
-        const int wi = wd[i], wj = wd[j];                                       \
-        key[i] = sw ? kj : ki; key[j] = sw ? ki : kj;                           \
-        wd[i] = sw ? wj : wi; wd[j] = sw ? wi : wj;                             \
-    }
-#else
 #define RTG_CSWAP(i, j)                                               \
     if (key[j] < key[i]) {                                           \
         const float tk = key[i]; key[i] = key[j]; key[j] = tk;      \
         const int tw = wd[i]; wd[i] = wd[j]; wd[j] = tw;             \
     }
-#endif
-#if RTG_WIDTH == 4
             RTG_CSWAP(0, 1) RTG_CSWAP(2, 3) RTG_CSWAP(0, 2) RTG_CSWAP(1, 3) RTG_CSWAP(1, 2)
-#else
-            RTG_CSWAP(0, 1) RTG_CSWAP(2, 3) RTG_CSWAP(4, 5) RTG_CSWAP(6, 7)
-            RTG_CSWAP(0, 2) RTG_CSWAP(1, 3) RTG_CSWAP(4, 6) RTG_CSWAP(5, 7)
-            RTG_CSWAP(1, 2) RTG_CSWAP(5, 6)
-            RTG_CSWAP(0, 4) RTG_CSWAP(1, 5) RTG_CSWAP(2, 6) RTG_CSWAP(3, 7)
-            RTG_CSWAP(2, 4) RTG_CSWAP(3, 5)
-            RTG_CSWAP(1, 2) RTG_CSWAP(3, 4) RTG_CSWAP(5, 6)
-#endif
 #undef RTG_CSWAP
             // misses carry +inf and sort last
             if (key[0] == __builtin_inff()) {
                 cur = RTG_POP;
-#if RTG_FAST_PUSH && RTG_WIDTH == 4
             } else if (!COUNT && sp + 3 <= RTG_STACK) {
                 // hits are a prefix of the sorted slots: push the h = hits - 1 far ones (far first)
                 // with three unconditional LDS writes; entries above sp + h are never read
@@ -376,10 +290,9 @@ void k_trace(SceneView s, TraceIO io) {
                 stk[sp + 2][tid] = wd[1];
                 sp += h;
                 cur = wd[0];
-#endif
             } else {
 #pragma unroll
-                for (int k = RTG_WIDTH - 1; k >= 1; --k) {
+                for (int k = 3; k >= 1; --k) {
                     if (key[k] != __builtin_inff()) {
                         if (COUNT && sp < RTG_STACK) kstk[sp][tid] = key[k];
                         if (sp < RTG_STACK) stk[sp][tid] = wd[k];
@@ -417,18 +330,11 @@ void k_trace(SceneView s, TraceIO io) {
                 cur = RTG_POP;
             }
         }
-#if RTG_POSTPONE
         // park a reached leaf (one per lane) and keep walking
         if (cur < 0 && cur != RTG_EXIT && cur != RTG_POP && pend == RTG_EXIT) {
             pend = cur;
             cur = RTG_POP;
         }
-#else
-        else if (cur != RTG_EXIT) {
-            leaf(cur);
-            cur = (anyr && occluded) ? RTG_EXIT : RTG_POP;
-        }
-#endif
         // ---- one pop for every branch: always an LDS read (ds_read, not a flat load through a
         // selected pointer); the global overflow read only for deep entries
         if (cur == RTG_POP) {
@@ -442,10 +348,10 @@ void k_trace(SceneView s, TraceIO io) {
                 if (sp >= RTG_STACK) cur = io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
             }
         }
-#if RTG_POSTPONE
-        // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on
+        // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on, or (the queue is
+        // dry) any parked leaf: the drain is latency-bound, lanes should not wait for each other
         const unsigned long long pm = __ballot(pend != RTG_EXIT);
-        if (__popcll(pm) >= RTG_POSTPONE || __ballot(cur >= 0) == 0 || (RTG_DRAIN_LEAF && drained && pm)) {
+        if (__popcll(pm) >= RTG_POSTPONE || __ballot(cur >= 0) == 0 || (drained && pm)) {
             if (COUNT) {
                 c_lslots += 64;
                 c_lstep += pend != RTG_EXIT ? 1 : 0;
@@ -459,9 +365,8 @@ void k_trace(SceneView s, TraceIO io) {
                 }
             }
         }
-#endif
     }
-    if (RTG_WAVETIME && io.wtime && lane == 0) io.wtime[3 * wslot + 2] = __builtin_amdgcn_s_memrealtime();
+    if (RTG_DEBUG && io.wtime && lane == 0) io.wtime[3 * wslot + 2] = __builtin_amdgcn_s_memrealtime();
     if (COUNT) {
         for (int off = 32; off > 0; off >>= 1) {
             c_nodes += __shfl_down(c_nodes, off);
@@ -492,182 +397,12 @@ void k_trace(SceneView s, TraceIO io) {
     }
 }
 
-// ------------------------------------------------------------------ coherent (camera) rays
-// Packet traversal for the camera rays of bounce 0: a wave takes 64 consecutive queue entries (at
-// bounce 0 the queue is the identity, so 64 neighbouring pixels of one 32x32 tile) and walks the
-// compressed 4-wide tree ONCE for all of them: one wave-uniform stack of (node, lane mask) in LDS,
-// node and triangle records fetched with scalar loads (no per-lane vector-memory requests, which
-// are what bounds the per-lane walk), every lane testing every slot against its own ray.
-// Exactness is unchanged: each lane still tests a superset of the nodes its own walk needs (a
-// slot is skipped only when no lane of the packet passes its conservative test), accepts a
-// candidate only if the exact reference leaf box passes, and keeps the (t, index) lexicographic
-// minimum. Lanes whose ray cannot use the compressed walk (a zero direction component) go to a
-// leftover queue that the per-lane k_trace finishes.
-// Measured on C3 (bounce-0 launch, 67M camera rays): 33.4 ms against 20.9 ms for the per-lane walk.
-// A packet is one dependent chain of scalar loads (6 per SIMD at 78 VGPRs) where the per-lane walk
-// keeps 384 chains in flight, so the walk is memory-latency bound; off by default (RTG_PACKET=1).
-#ifndef RTG_PSTACK
-#define RTG_PSTACK 96
-#endif
-// record loads through the constant address space: uniform addresses become scalar loads
-typedef __attribute__((address_space(4))) const float cfloat;
-static __device__ __forceinline__ float4 cload4(const void* base, int i) {
-    cfloat* q = (cfloat*)base + 4 * i;
-    return make_float4(q[0], q[1], q[2], q[3]);
-}
-
-__global__ __launch_bounds__(RTG_TB) void k_trace_packet(SceneView s, TraceIO io, unsigned* left_q, unsigned* left_n) {
-    __shared__ int pw[RTG_TB / 64][RTG_PSTACK];
-    __shared__ unsigned long long pm[RTG_TB / 64][RTG_PSTACK];
-    const int lane = lane_id();
-    const int wv = threadIdx.x >> 6;
-    const unsigned n = *io.count;
-    for (;;) {
-        unsigned g = 0;
-        if (lane == 0) g = atomicAdd(io.fetch, 64u);
-        g = __builtin_amdgcn_readfirstlane(__shfl(g, 0));
-        if (g >= n) break;
-        const unsigned ri = g + lane;
-        bool have = ri < n;
-        const int pid = have ? (int)io.queue[ri] : 0;
-        const float4 ro = io.ray_o[pid], rd = io.ray_d[pid];
-        const v3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
-        const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // Ray::init
-        const bool wide = fabsf(inv.x) <= 0x1p64f && fabsf(inv.y) <= 0x1p64f && fabsf(inv.z) <= 0x1p64f &&
-                          inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
-        if (have && !wide) {  // per-lane walk (BVH2) for these
-            left_q[atomicAdd(left_n, 1u)] = (unsigned)pid;
-            have = false;
-        }
-        float tbest = RTG_FLT_MAX, bu = 0.0f, bv = 0.0f;
-        int bid = -1;
-        const float omag = s.cull_scale + fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-        const float dmag = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
-        float delta = RTG_CULL_REL * omag;
-        const float mu = RTG_CULL_REL * omag;
-        const float imax = fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z));
-        const bool px = inv.x > 0.0f, py = inv.y > 0.0f, pz = inv.z > 0.0f;
-        const float mnx = px ? -mu : mu, mny = py ? -mu : mu, mnz = pz ? -mu : mu;
-        const float* rb = s.root_box;
-        const unsigned long long root = __ballot(have && slab_exact(rb[0], rb[1], rb[2], rb[3], rb[4], rb[5], o, inv));
-        int sp = 0;
-        if (root) {
-            if (lane == 0) {
-                pw[wv][0] = s.root_wordw;
-                pm[wv][0] = root;
-            }
-            sp = 1;
-        }
-        // leaf (1-2 triangles) for the lanes of mask m; records through scalar loads
-        auto leaf = [&](int word, unsigned long long m) {
-            const int code = ~word;
-            const int start = code / RTG_LEAF_SPAN;  // leaf word ~(start * RTG_LEAF_SPAN + count - 1)
-            const int cnt = (code % RTG_LEAF_SPAN) + 1;
-            const bool mine = (m >> lane) & 1ull;
-            for (int k = 0; k < cnt; ++k) {
-                const int tri = start + k;
-                DevTri48 T;
-                T.a = cload4(s.tris48 + tri, 0);
-                T.b = cload4(s.tris48 + tri, 1);
-                T.c = cload4(s.tris48 + tri, 2);
-                float t, u, v;
-                if (!mine) continue;
-                const bool hit = tri_intersect48(T, o, d, [&](float tt) { return tt <= tbest && tt > RTG_EPS; }, t, u, v);
-                if (hit && t > RTG_EPS && (t < tbest || (t == tbest && tri < bid))) {
-                    const float4 b0 = cload4(s.leafbox + 2 * tri, 0), b1 = cload4(s.leafbox + 2 * tri, 1);
-                    if (slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv)) {
-                        tbest = t;
-                        bid = tri;
-                        bu = u;
-                        bv = v;
-                        delta = RTG_CULL_REL * (omag + tbest * dmag);
-                    }
-                }
-            }
-        };
-        while (sp > 0) {
-            --sp;
-            const int w = __builtin_amdgcn_readfirstlane(pw[wv][sp]);
-            const unsigned long long m = pm[wv][sp];
-            const unsigned mlo = __builtin_amdgcn_readfirstlane((unsigned)m);
-            const unsigned mhi = __builtin_amdgcn_readfirstlane((unsigned)(m >> 32));
-            const unsigned long long mm = ((unsigned long long)mhi << 32) | mlo;
-            if (w < 0) {
-                leaf(w, mm);
-                continue;
-            }
-            const float4 h0 = cload4(s.nodesq + w, 0), h1 = cload4(s.nodesq + w, 1), h2 = cload4(s.nodesq + w, 2),
-                         h3 = cload4(s.nodesq + w, 3);
-            const unsigned ex = __float_as_uint(h0.w);
-            const float sx = __uint_as_float((ex & 255u) << 23);
-            const float sy = __uint_as_float(((ex >> 8) & 255u) << 23);
-            const float sz = __uint_as_float(((ex >> 16) & 255u) << 23);
-            const unsigned p0 = __float_as_uint(h1.x), p1 = __float_as_uint(h1.y), p2 = __float_as_uint(h1.z);
-            const unsigned p3 = __float_as_uint(h1.w), p4 = __float_as_uint(h2.x), p5 = __float_as_uint(h2.y);
-            const int wd[4] = {__float_as_int(h2.z), __float_as_int(h2.w), __float_as_int(h3.x), __float_as_int(h3.y)};
-            // the per-lane conservative slot test of k_trace (same margins)
-            const unsigned nqx = px ? p0 : p3, fqx = px ? p3 : p0;
-            const unsigned nqy = py ? p1 : p4, fqy = py ? p4 : p1;
-            const unsigned nqz = pz ? p2 : p5, fqz = pz ? p5 : p2;
-            const float ax0 = ((h0.x + mnx) - o.x) * inv.x, ax1 = ((h0.x - mnx) - o.x) * inv.x;
-            const float ay0 = ((h0.y + mny) - o.y) * inv.y, ay1 = ((h0.y - mny) - o.y) * inv.y;
-            const float az0 = ((h0.z + mnz) - o.z) * inv.z, az1 = ((h0.z - mnz) - o.z) * inv.z;
-            const float six = sx * inv.x, siy = sy * inv.y, siz = sz * inv.z;
-            const float cshift = (delta - mu) * imax;
-            const bool mine = (mm >> lane) & 1ull;
-            unsigned long long hm[4];
-            float key[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float tnx = fmaf((float)((nqx >> (8 * k)) & 255u), six, ax0);
-                const float tny = fmaf((float)((nqy >> (8 * k)) & 255u), siy, ay0);
-                const float tnz = fmaf((float)((nqz >> (8 * k)) & 255u), siz, az0);
-                const float tfx = fmaf((float)((fqx >> (8 * k)) & 255u), six, ax1);
-                const float tfy = fmaf((float)((fqy >> (8 * k)) & 255u), siy, ay1);
-                const float tfz = fmaf((float)((fqz >> (8 * k)) & 255u), siz, az1);
-                const float en = fmaxf(fmaxf(tnx, tny), tnz);
-                const float tx = fminf(fminf(tfx, tfy), tfz);
-                const float e = en - cshift;
-                const bool hit = mine & (wd[k] != RTG_EXIT) & !((tx < en) | (tx < 0.0f)) & (!io.cull | !(e > tbest));
-                hm[k] = __ballot(hit);
-                key[k] = e;
-            }
-            // push the hit slots far-to-near by the entry distance of the packet's first lane that
-            // hits them; leaf slots last, so they are popped (and lower tbest) first
-            int ord[4];
-            float ok[4];  // sort keys (wave-uniform)
-            int nh = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (!hm[k]) continue;
-                ord[nh] = k;
-                ok[nh] = wd[k] < 0 ? -RTG_FLT_MAX
-                                   : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(key[k]), __builtin_ctzll(hm[k])));
-                ++nh;
-            }
-            for (int a = 1; a < nh; ++a)  // insertion sort, descending key
-                for (int b = a; b > 0 && ok[b] > ok[b - 1]; --b) {
-                    const float tk = ok[b]; ok[b] = ok[b - 1]; ok[b - 1] = tk;
-                    const int to = ord[b]; ord[b] = ord[b - 1]; ord[b - 1] = to;
-                }
-            for (int a = 0; a < nh; ++a) {
-                if (lane == 0) {
-                    pw[wv][sp] = wd[ord[a]];
-                    pm[wv][sp] = hm[ord[a]];
-                }
-                ++sp;
-            }
-        }
-        if (have) io.hits[pid] = make_float4(tbest, __int_as_float(bid), bu, bv);
-    }
-}
-
 // ------------------------------------------------------------------ generate
 __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
     const unsigned pid = blockIdx.x * blockDim.x + threadIdx.x;
     if (pid == 0) p.ctr[0].n_ext = a.P;
     if (pid >= a.P) return;
-    const unsigned lp = a.pm ? pid / a.ns : pid % a.npix, sl = a.pm ? pid % a.ns : pid / a.npix;
+    const unsigned lp = pid / a.ns, sl = pid % a.ns;  // pixel-major path ids
     const unsigned pixel = a.pixlist[lp];
     const unsigned W = (unsigned)a.cam.width;
     const unsigned x = pixel % W, y = pixel / W;
@@ -702,13 +437,6 @@ template <bool ALT>
 __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
     __shared__ unsigned s_cnt[2][RTG_TB / 64];
     __shared__ unsigned s_base[2];
-#if RTG_SHADE_SORT
-    __shared__ int s_sort[RTG_TB];
-#endif
-#if RTG_SHADE_BUF
-    __shared__ unsigned s_q[2][RTG_SHADE_BUF];
-    unsigned fill_e = 0, fill_s = 0;  // block-uniform fill of the LDS id buffers
-#endif
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     const unsigned n = p.ctr[b].n_ext;
@@ -716,56 +444,15 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
     unsigned* qout = p.q[(b + 1) & 1];
     float4* contrib = p.contrib + (size_t)b * a.P;
     const bool lean0 = a.lean && b == 0;  // bounce 0: identity queue, state as k_generate would write it
-    // block-uniform loop: all waves of a block take part in every compaction round
-#if RTG_SHADE_PF
-    // the next iteration's path id is loaded one iteration ahead (it heads the dependent chain
-    // id -> payload -> shading record -> texture)
-    unsigned pf_i = blockIdx.x * RTG_TB + threadIdx.x;
-    int pid_next = pf_i < n ? (int)qin[pf_i] : 0;
-#endif
+    // block-uniform loop: all waves of a block take part in every compaction round (the launch has
+    // one 256-path tile per block: a finished block frees its slot for the next tile)
     for (unsigned base = blockIdx.x * RTG_TB; base < n; base += gridDim.x * RTG_TB) {
         const unsigned i = base + threadIdx.x;
         int pid = 0;
-#if RTG_SHADE_PF
-        pid = pid_next;
-        pf_i = i + gridDim.x * RTG_TB;
-        pid_next = pf_i < n ? (int)qin[pf_i] : 0;
-#endif
         bool want_ext = false, want_sh = false;
-        bool valid = i < n;
-#if RTG_SHADE_SORT
-        {
-            // stable block-level partition of the 256 path ids: misses first, then hits, so that
-            // waves run the miss branch (background lookup) and the surface branch without lane
-            // divergence between them (at most one wave holds both)
-            const int p0 = valid ? (lean0 ? (int)i : (int)qin[i]) : 0;
-            const bool miss = valid && !(p.hits[p0].x < RTG_FLT_MAX);
-            const unsigned long long mm = __ballot(miss), mh = __ballot(valid && !miss);
-            if (lane == 0) {
-                s_cnt[0][wave] = (unsigned)__popcll(mm);
-                s_cnt[1][wave] = (unsigned)__popcll(mh);
-            }
-            __syncthreads();
-            unsigned nm = 0, om = 0, oh = 0, nv = 0;
-            for (int w = 0; w < RTG_TB / 64; ++w) {
-                if (w < wave) {
-                    om += s_cnt[0][w];
-                    oh += s_cnt[1][w];
-                }
-                nm += s_cnt[0][w];
-                nv += s_cnt[0][w] + s_cnt[1][w];
-            }
-            if (miss) s_sort[om + prefix_lt(mm)] = p0;
-            else if (valid) s_sort[nm + oh + prefix_lt(mh)] = p0;
-            __syncthreads();
-            valid = threadIdx.x < nv;
-            pid = valid ? s_sort[threadIdx.x] : 0;
-        }
-#endif
+        const bool valid = i < n;
         if (valid) {
-#if !RTG_SHADE_SORT && !RTG_SHADE_PF
             pid = lean0 ? (int)i : (int)qin[i];
-#endif
             const float4 ro = lean0 ? make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f) : p.ray_o[pid];
             const float4 rd = p.ray_d[pid];
             const float4 h = p.hits[pid];
@@ -773,8 +460,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             const float4 thr4 = lean0 ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : p.thr[pid];
             v3 thr = mk(thr4.x, thr4.y, thr4.z);
             const int can_hit = lean0 ? 1 : (p.meta[pid] >> 8) & 1;
-            const unsigned lp = a.pm ? (unsigned)pid / a.ns : (unsigned)pid % a.npix;
-            const unsigned sl = a.pm ? (unsigned)pid % a.ns : (unsigned)pid / a.npix;
+            const unsigned lp = (unsigned)pid / a.ns, sl = (unsigned)pid % a.ns;
             const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);
             uint64_t st = lean0 ? pcg_seed(a.seed, inc) : p.rng[pid];
             v3 c;
@@ -920,7 +606,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                     const v3 alb = tex_sample(s, M, tu, tv);
                     // ---- computeDirect (Renderer.h:423-473)
                     v3 ld = mk(0.0f, 0.0f, 0.0f);
-                    bool ld_pre = false;  // contrib takes the visible NEE value now (RTG_SHC_SPEC)
+                    bool ld_pre = false;  // contrib takes the visible NEE value now
                     v3 cpre = ld;
                     if (!spec) {
                         const int nl = s.n_lights;
@@ -968,7 +654,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                             // writes thr * 0 = +0 on occlusion. When thr * 0 is not +0 (a non-finite
                             // throughput) the value goes through sh_c and is copied on visibility.
                             const v3 z = mul(thr, mk(0.0f, 0.0f, 0.0f));
-                            const bool plain = RTG_SHC_SPEC && (__float_as_uint(z.x) | __float_as_uint(z.y) | __float_as_uint(z.z)) == 0u;
+                            const bool plain = (__float_as_uint(z.x) | __float_as_uint(z.y) | __float_as_uint(z.z)) == 0u;
                             p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, plain ? 0.0f : 1.0f);
                             if (!plain) p.sh_c[pid] = make_float4(cvis.x, cvis.y, cvis.z, 0.0f);
                             ld_pre = plain;
@@ -1013,48 +699,6 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             s_cnt[1][wave] = (unsigned)__popcll(ms);
         }
         __syncthreads();
-#if RTG_SHADE_BUF
-        {
-            // stage the ids in LDS; append a buffer to its queue (one atomic) once another
-            // iteration might not fit, and at the block's last iteration
-            unsigned oe = fill_e, os = fill_s, te = 0, ts = 0;
-            for (int w = 0; w < RTG_TB / 64; ++w) {
-                if (w < wave) {
-                    oe += s_cnt[0][w];
-                    os += s_cnt[1][w];
-                }
-                te += s_cnt[0][w];
-                ts += s_cnt[1][w];
-            }
-            if (want_ext) s_q[0][oe + prefix_lt(me)] = (unsigned)pid;
-            if (want_sh) s_q[1][os + prefix_lt(ms)] = (unsigned)pid;
-            fill_e += te;
-            fill_s += ts;
-            const bool last = base + gridDim.x * RTG_TB >= n;
-            const bool fe = fill_e > RTG_SHADE_BUF - RTG_TB || (last && fill_e);
-            const bool fs = fill_s > RTG_SHADE_BUF - RTG_TB || (last && fill_s);
-            __syncthreads();
-            if (fe || fs) {
-                if (threadIdx.x == 0) {
-                    s_base[0] = fe ? atomicAdd(&p.ctr[b + 1].n_ext, fill_e) : 0u;
-                    s_base[1] = fs ? atomicAdd(&p.ctr[b].n_shadow, fill_s) : 0u;
-                }
-                __syncthreads();
-                if (fe) {
-                    const unsigned ob = s_base[0];
-                    for (unsigned j = threadIdx.x; j < fill_e; j += RTG_TB) qout[ob + j] = s_q[0][j];
-                    fill_e = 0;
-                }
-                if (fs) {
-                    const unsigned ob = s_base[1];
-                    for (unsigned j = threadIdx.x; j < fill_s; j += RTG_TB) p.shq[ob + j] = s_q[1][j];
-                    fill_s = 0;
-                }
-                __syncthreads();
-            }
-            continue;
-        }
-#endif
         if (threadIdx.x == 0) {
             unsigned te = 0, ts = 0;
             for (int w = 0; w < RTG_TB / 64; ++w) {
@@ -1083,7 +727,7 @@ __global__ __launch_bounds__(RTG_TB) void k_accumulate(ChunkArgs a, PathBufs p, 
     const unsigned pixel = a.pixlist[lp];
     float fr = film[(size_t)pixel * 3 + 0], fg = film[(size_t)pixel * 3 + 1], fb = film[(size_t)pixel * 3 + 2];
     for (unsigned sl = 0; sl < a.ns; ++sl) {
-        const unsigned pid = a.pm ? lp * a.ns + sl : sl * a.npix + lp;
+        const unsigned pid = lp * a.ns + sl;
         const int nt = p.meta[pid] & 0xff;
         float4 acc = p.contrib[(size_t)(nt - 1) * a.P + pid];
         for (int j = nt - 2; j >= 0; --j) {
@@ -1099,7 +743,7 @@ __global__ __launch_bounds__(RTG_TB) void k_accumulate(ChunkArgs a, PathBufs p, 
     film[(size_t)pixel * 3 + 2] = fb;
 }
 
-// Pixel-major chunks (pid = lp * ns + sl): one wave per pixel, lane = sample, so the contrib reads
+// Several samples per pixel (pid = lp * ns + sl): one wave per pixel, lane = sample, so the contrib reads
 // are contiguous. Each lane folds its path's right-nested sum; then lanes 0-2 (R, G, B) add the
 // samples to the film in sample order from LDS: the same additions in the same order as
 // k_accumulate, so the same bits.
@@ -1197,21 +841,21 @@ __global__ void k_tally(const Counters* ctr, int maxb, unsigned long long* stats
 
 // ================================================================== host side (C-ABI)
 thread_local std::string g_err;
-static void free_chunk(rtg_handle* h, int i) {
-    PathBufs& p = h->pb[i];
+static void free_chunk(rtg_handle* h) {
+    PathBufs& p = h->pb;
     (void)hipFree(p.thr); (void)hipFree(p.rng); (void)hipFree(p.meta); (void)hipFree(p.contrib);
     (void)hipFree(p.q[0]); (void)hipFree(p.q[1]); (void)hipFree(p.hits); (void)hipFree(p.shq); (void)hipFree(p.ctr);
     (void)hipFree(p.ray_o); (void)hipFree(p.ray_d);
     (void)hipFree(p.sh_o); (void)hipFree(p.sh_d); (void)hipFree(p.sh_c);
     p = PathBufs{};
-    h->cap_P[i] = 0;
-    h->cap_maxb[i] = 0;
+    h->cap_P = 0;
+    h->cap_maxb = 0;
 }
 
-int ensure_chunk(rtg_handle* h, int i, size_t P, int maxb) {
-    if (P <= h->cap_P[i] && maxb <= h->cap_maxb[i]) return RTG_OK;
-    free_chunk(h, i);
-    PathBufs& p = h->pb[i];
+int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
+    if (P <= h->cap_P && maxb <= h->cap_maxb) return RTG_OK;
+    free_chunk(h);
+    PathBufs& p = h->pb;
     HIPOK(hipMalloc((void**)&p.thr, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.rng, P * sizeof(unsigned long long)));
     HIPOK(hipMalloc((void**)&p.meta, P * sizeof(int)));
@@ -1226,18 +870,18 @@ int ensure_chunk(rtg_handle* h, int i, size_t P, int maxb) {
     HIPOK(hipMalloc((void**)&p.sh_d, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.sh_c, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.ctr, (size_t)(maxb + 1) * sizeof(Counters)));
-    h->cap_P[i] = P;
-    h->cap_maxb[i] = maxb;
+    h->cap_P = P;
+    h->cap_maxb = maxb;
     return RTG_OK;
 }
 
 int ensure_ovf(rtg_handle* h) {
     int grid = std::max(h->trace_blocks, h->trace_blocks_count);
-    // deepest stack: one entry per BVH2 level, or up to RTG_WIDTH-1 per wide level (each wide
-    // level descends at least one BVH2 level)
-    size_t deep = std::max<size_t>(h->bvh_depth, (size_t)h->wide_depth * (RTG_WIDTH - 1)) + 2;
+    // deepest stack: one entry per BVH2 level, or up to 3 per wide level (each wide level descends
+    // at least one BVH2 level)
+    size_t deep = std::max<size_t>(h->bvh_depth, (size_t)h->wide_depth * 3) + 2;
     size_t levels = deep > RTG_STACK ? deep - RTG_STACK : 1;
-    size_t need = 2 * levels * (size_t)grid * RTG_TB;  // one region per chunk pipeline
+    size_t need = levels * (size_t)grid * RTG_TB;
     if (need <= h->cap_ovf) return RTG_OK;
     (void)hipFree(h->d_ovf);
     HIPOK(hipMalloc((void**)&h->d_ovf, need * sizeof(int)));
@@ -1258,14 +902,6 @@ static bool encode_qnode(const float* bounds, const std::vector<int>& slots, con
         for (int k = 1; k < (int)slots.size(); ++k) {
             lo[a] = std::min(lo[a], bounds[(size_t)slots[k] * 6 + a]);
             hi[a] = std::max(hi[a], bounds[(size_t)slots[k] * 6 + 3 + a]);
-        }
-        if (RTG_NODE48) {  // origin rounded down to a 16-bit mantissa (its low byte holds the exponent)
-            uint32_t b;
-            std::memcpy(&b, &lo[a], 4);
-            if ((int32_t)b >= 0) b &= ~0xffu;
-            else b = (b + 0xffu) & ~0xffu;
-            std::memcpy(&lo[a], &b, 4);
-            if (!std::isfinite(lo[a])) return false;
         }
     }
     unsigned planes[6] = {0, 0, 0, 0, 0, 0};
@@ -1295,30 +931,10 @@ static bool encode_qnode(const float* bounds, const std::vector<int>& slots, con
         }
     }
     auto uf = [](unsigned v) { float f; std::memcpy(&f, &v, 4); return f; };
-#if RTG_NODE48
-    unsigned w24[4];
-    for (int k = 0; k < 4; ++k) {
-        const int w = words[k];
-        if (w == RTG_EXIT) w24[k] = 0xffffffu;
-        else if (w < 0) {
-            if ((unsigned)~w >= 0x7fffffu) return false;  // leaf code must fit 23 bits
-            w24[k] = (unsigned)~w | 0x800000u;
-        } else {
-            if ((unsigned)w >= 0x800000u) return false;   // node index must fit 23 bits
-            w24[k] = (unsigned)w;
-        }
-    }
-    auto ob = [&](int a) { uint32_t b; std::memcpy(&b, &lo[a], 4); return b | bexp[a]; };
-    out.q[0] = make_float4(uf(ob(0)), uf(ob(1)), uf(ob(2)), uf(planes[0]));
-    out.q[1] = make_float4(uf(planes[1]), uf(planes[2]), uf(planes[3]), uf(planes[4]));
-    out.q[2] = make_float4(uf(planes[5]), uf(w24[0] | (w24[1] << 24)), uf((w24[1] >> 8) | (w24[2] << 16)),
-                           uf((w24[2] >> 16) | (w24[3] << 8)));
-#else
     out.q[0] = make_float4(lo[0], lo[1], lo[2], uf(bexp[0] | (bexp[1] << 8) | (bexp[2] << 16)));
     out.q[1] = make_float4(uf(planes[0]), uf(planes[1]), uf(planes[2]), uf(planes[3]));
     out.q[2] = make_float4(uf(planes[4]), uf(planes[5]), host_bits_f(words[0]), host_bits_f(words[1]));
     out.q[3] = make_float4(host_bits_f(words[2]), host_bits_f(words[3]), 0.0f, 0.0f);
-#endif
     return true;
 }
 static float host_dot(const float* a, const float* b) { return ((a[0] * b[0]) + (a[1] * b[1])) + (a[2] * b[2]); }
@@ -1328,7 +944,7 @@ static void host_cross(const float* a, const float* b, float* o) {
     o[2] = (a[0] * b[1]) - (a[1] * b[0]);
 }
 
-// Own binary SAH tree over the reference's leaves (RTG_REBUILD=1), in the descriptor's node format
+// Own binary SAH tree over the reference's leaves, in the descriptor's node format
 // (links {left, right, start, end}, bounds {min xyz, max xyz}; node 0 is the root). Primitives are
 // the reference leaves with their exact boxes, kept whole, so the wide walk built from this tree
 // still reaches every leaf whose box passes (internal boxes are float min/max unions: containment
@@ -1356,18 +972,13 @@ static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& l
             return x * y + y * z + z * x;
         }
     };
-    // SAH weight of a leaf: its triangle count (1-2), or 1 per leaf (RTG_RB_WEIGHT=0); full sweep
-    // below RTG_RB_SWEEP leaves, RTG_RB_BINS centroid bins per axis above
-    const char* ew = std::getenv("RTG_RB_WEIGHT");
-    const char* es = std::getenv("RTG_RB_SWEEP");
-    const char* eb = std::getenv("RTG_RB_BINS");
-    const bool by_tris = ew ? std::atoi(ew) != 0 : true;
-    const int sweep_max = es ? std::max(2, std::atoi(es)) : 2048;
-    const int nbins = eb ? std::min(256, std::max(4, std::atoi(eb))) : 64;
+    // SAH weight of a leaf: its triangle count (1-2); full sweep below 2048 leaves, 64 centroid
+    // bins per axis above (a full sweep to 16384 leaves or 256 bins measured no better)
+    const int sweep_max = 2048, nbins = 64;
     std::vector<double> wt(n), pre;
     for (size_t p = 0; p < n; ++p) {
         const int32_t* L = d->node_links + (size_t)leaf[p] * 4;
-        wt[p] = by_tris ? (double)(L[3] - L[2]) : 1.0;
+        wt[p] = (double)(L[3] - L[2]);
     }
     std::vector<int> idx(n);
     for (size_t p = 0; p < n; ++p) idx[p] = (int)p;
@@ -1487,15 +1098,13 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     }
     h->device = device;
     HIPOK(hipSetDevice(device));
-    if (std::getenv("RTG_NULL_STREAM")) h->stream = nullptr;  // legacy default stream (profiling aid)
-    else HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     HIPOK(hipGetDeviceProperties(&prop, device));
     h->n_cu = prop.multiProcessorCount;
     const uint32_t nt = d->n_tris;
 
     // ---- triangles: Triangle::init (Geometry.h:72-83) + gNormal (:127-130)
-    std::vector<DevTri> tris(nt);
     std::vector<DevTri48> tris48(nt);
     std::vector<DevShade> shade(nt);
     std::vector<float> tri_area(nt), tri_gn(nt * 3);
@@ -1508,16 +1117,10 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         host_cross(e1, e2, c);
         float l = 1.0f / std::sqrt(((c[0] * c[0]) + (c[1] * c[1])) + (c[2] * c[2]));
         float n[3] = {c[0] * l, c[1] * l, c[2] * l};
-        float dd = host_dot(n, v0);
-        float inv_area = 1.0f / host_dot(c, n);
         tri_area[i] = std::sqrt(((c[0] * c[0]) + (c[1] * c[1])) + (c[2] * c[2])) * 0.5f;
         const float* N = d->normals + (size_t)i * 9;
         float s = host_dot(N, n) > 0 ? 1.0f : -1.0f;
         for (int k = 0; k < 3; ++k) tri_gn[i * 3 + k] = n[k] * s;
-        tris[i].nd = make_float4(n[0], n[1], n[2], dd);
-        tris[i].v1i = make_float4(v1[0], v1[1], v1[2], inv_area);
-        tris[i].v2 = make_float4(v2[0], v2[1], v2[2], 0.0f);
-        tris[i].e2 = make_float4(e2[0], e2[1], e2[2], 0.0f);
         tris48[i].a = make_float4(n[0], n[1], n[2], v0[0]);
         tris48[i].b = make_float4(v0[1], v0[2], v1[0], v1[1]);
         tris48[i].c = make_float4(v1[2], v2[0], v2[1], v2[2]);
@@ -1578,7 +1181,6 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     // ---- wide collapse: each node's slots are a cut of the BVH2 subtree below it, grown by
     // repeatedly opening the internal slot of largest surface area (leaves stay slots). Exact
     // boxes are kept, so reachability is the reference's (see k_trace).
-    std::vector<DevNodeW> nodesw;
     std::vector<DevNodeQ> nodesq;
     bool qok = true;
     int root_wordw = root_word;
@@ -1596,12 +1198,11 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         }
     }
     if (nt > 0 && finite && d->node_links[0] >= 0) {
-        // the tree the wide nodes are cut from: the reference BVH2, or (RTG_REBUILD=1) an own SAH
-        // tree over the reference's leaves (rebuild_over_leaves)
+        // the tree the wide nodes are cut from: an own SAH tree over the reference's leaves
+        // (rebuild_over_leaves), or the reference BVH2 when that tree cannot be built
         std::vector<int32_t> rlk;
         std::vector<float> rbd;
-        const char* rb_env = std::getenv("RTG_REBUILD");
-        const bool rebuilt = (rb_env ? std::atoi(rb_env) != 0 : RTG_REBUILD) && rebuild_over_leaves(d, rlk, rbd);
+        const bool rebuilt = rebuild_over_leaves(d, rlk, rbd);
         const int32_t* LK = rebuilt ? rlk.data() : d->node_links;
         const float* BD = rebuilt ? rbd.data() : d->node_bounds;
         const uint32_t nn = rebuilt ? (uint32_t)(rlk.size() / 4) : d->n_nodes;
@@ -1619,89 +1220,11 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             const double x = b[3] - b[0], y = b[4] - b[1], z = b[5] - b[2];
             return x * y + y * z + z * x;
         };
-        // SAH-optimal cut (RTG_COLLAPSE=dp): bottom-up over the BVH2, best[n][k] is the
-        // least expected cost of covering n's subtree with at most k slots, a slot being a
-        // reference leaf, a wide node, or (leaf merge) a subtree of <= RTG_LEAF_SPAN triangles
-        // tested as one leaf; cost = area x (node step | triangles x c_tri). Every slot box still
-        // contains the reference leaf boxes below it, so the exactness argument of k_trace holds.
-        const char* ce = std::getenv("RTG_COLLAPSE");
-        const bool dp = ce ? std::strcmp(ce, "dp") == 0 : RTG_COLLAPSE_DP;
-        const double c_tri = std::getenv("RTG_DP_CTRI") ? std::atof(std::getenv("RTG_DP_CTRI")) : 0.6;
-        const int leaf_max = std::getenv("RTG_DP_LEAF") ? std::atoi(std::getenv("RTG_DP_LEAF")) : RTG_LEAF_SPAN;
-        std::vector<std::array<double, 5>> best;
-        std::vector<std::array<int8_t, 5>> split;  // k >= 2: 0 = as k-1, j = j slots left / k-j right
-        std::vector<int8_t> wsplit, merged;         // wide node: slots given to the left child; merged leaf
-        std::vector<int> lo_tri, n_tri;
-        if (dp) {
-            best.assign(nn, {});
-            split.assign(nn, {});
-            wsplit.assign(nn, 0);
-            merged.assign(nn, 0);
-            lo_tri.assign(nn, 0);
-            n_tri.assign(nn, 0);
-            std::vector<int> order;  // post-order (children first)
-            order.reserve(nn);
-            std::vector<std::pair<int, bool>> st{{0, false}};
-            while (!st.empty()) {
-                auto [i, done] = st.back();
-                st.pop_back();
-                if (done || !internal(i)) { order.push_back(i); continue; }
-                st.push_back({i, true});
-                st.push_back({LK[(size_t)i * 4 + 1], false});
-                st.push_back({LK[(size_t)i * 4], false});
-            }
-            for (int i : order) {
-                const int32_t* L = LK + (size_t)i * 4;
-                const double A = area(i);
-                if (!internal(i)) {
-                    lo_tri[i] = L[2];
-                    n_tri[i] = L[3] - L[2];
-                    for (int k = 1; k <= 4; ++k) best[i][k] = A * c_tri * n_tri[i];
-                    continue;
-                }
-                const int l = L[0], r = L[1];
-                lo_tri[i] = std::min(lo_tri[l], lo_tri[r]);
-                n_tri[i] = n_tri[l] + n_tri[r];
-                const bool contiguous = std::max(lo_tri[l] + n_tri[l], lo_tri[r] + n_tri[r]) - lo_tri[i] == n_tri[i];
-                double cw = 1e300;
-                for (int j = 1; j <= 3; ++j) {
-                    const double c = best[l][j] + best[r][4 - j];
-                    if (c < cw) { cw = c; wsplit[i] = (int8_t)j; }
-                }
-                cw += A;  // one node step
-                double c1 = cw;
-                if (i != 0 && contiguous && n_tri[i] <= leaf_max && A * c_tri * n_tri[i] < cw) {
-                    c1 = A * c_tri * n_tri[i];
-                    merged[i] = 1;
-                }
-                best[i][1] = c1;
-                for (int k = 2; k <= 4; ++k) {
-                    best[i][k] = best[i][k - 1];
-                    for (int j = 1; j < k; ++j) {
-                        const double c = best[l][j] + best[r][k - j];
-                        if (c < best[i][k]) { best[i][k] = c; split[i][k] = (int8_t)j; }
-                    }
-                }
-            }
-        }
         // the slots of the wide node made from BVH2 node n2: a cut of its subtree below it
         auto cut = [&](int n2) {
             std::vector<int> slots;
-            if (dp) {
-                std::vector<std::pair<int, int>> st{{LK[(size_t)n2 * 4 + 1], 4 - wsplit[n2]},
-                                                    {LK[(size_t)n2 * 4], wsplit[n2]}};
-                while (!st.empty()) {
-                    auto [x, k] = st.back();
-                    st.pop_back();
-                    while (k > 1 && split[x][k] == 0) --k;
-                    if (k == 1) { slots.push_back(x); continue; }
-                    st.push_back({LK[(size_t)x * 4 + 1], k - split[x][k]});
-                    st.push_back({LK[(size_t)x * 4], split[x][k]});
-                }
-                return slots;
-            }
             slots = {LK[(size_t)n2 * 4], LK[(size_t)n2 * 4 + 1]};
-            while ((int)slots.size() < RTG_WIDTH) {
+            while ((int)slots.size() < 4) {
                 int best_k = -1;
                 for (int k = 0; k < (int)slots.size(); ++k)
                     if (internal(slots[k]) && (best_k < 0 || area(slots[k]) > area(slots[best_k]))) best_k = k;
@@ -1712,7 +1235,6 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             }
             return slots;
         };
-        nodesw.emplace_back();
         nodesq.emplace_back();
         root_wordw = 0;
         std::vector<std::array<int, 3>> work{{0, 0, 1}};  // BVH2 node, wide node, wide level
@@ -1721,12 +1243,9 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             work.pop_back();
             h->wide_depth = std::max(h->wide_depth, (uint32_t)lvl);
             const std::vector<int> slots = cut(n2);
-#if RTG_QNODE
             int32_t wq[4] = {RTG_EXIT, RTG_EXIT, RTG_EXIT, RTG_EXIT};
             for (int k = 0; k < (int)slots.size(); ++k) {
-                if (dp && merged[slots[k]]) {  // one leaf slot for a small subtree
-                    wq[k] = ~(lo_tri[slots[k]] * RTG_LEAF_SPAN + (n_tri[slots[k]] - 1));
-                } else if (internal(slots[k])) {
+                if (internal(slots[k])) {
                     wq[k] = (int)nodesq.size();
                     nodesq.emplace_back();
                     work.push_back({slots[k], wq[k], lvl + 1});
@@ -1736,43 +1255,22 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
                 }
             }
             if (!encode_qnode(BD, slots, wq, nodesq[nw])) { qok = false; break; }
-            continue;
-#endif
-            float f[RTG_WNODE_F4 * 4];
-            int32_t* wdw = reinterpret_cast<int32_t*>(f + 6 * RTG_WIDTH);
-            for (int k = 0; k < RTG_WNODE_F4 * 4; ++k) f[k] = 0.0f;
-            for (int k = 0; k < RTG_WIDTH; ++k) wdw[k] = RTG_EXIT;
-            for (int k = 0; k < (int)slots.size(); ++k) {
-                const float* bb = BD + (size_t)slots[k] * 6;
-                for (int q = 0; q < 6; ++q) f[q * RTG_WIDTH + k] = bb[q];
-                if (internal(slots[k])) {
-                    wdw[k] = (int)nodesw.size();
-                    nodesw.emplace_back();
-                    work.push_back({slots[k], wdw[k], lvl + 1});
-                } else if (!wordw(slots[k], wdw[k])) {
-                    g_err = "bad BVH leaf";
-                    return RTG_ERR_ARG;
-                }
-            }
-            std::memcpy(&nodesw[nw], f, sizeof(DevNodeW));
         }
     }
     float cull_scale = 0.0f;
     for (int k = 0; k < 6; ++k)
         if (std::isfinite(d->node_bounds[k])) cull_scale = std::max(cull_scale, std::fabs(d->node_bounds[k]));
     // the compressed walk's rounding margin is stated relative to the scene scale (k_trace)
-    h->usew = finite && qok && nt > 0 && (!RTG_QNODE || (cull_scale >= 0x1p-60f && cull_scale <= 0x1p60f));
+    h->usew = finite && qok && nt > 0 && cull_scale >= 0x1p-60f && cull_scale <= 0x1p60f;
     // exact leaf boxes per triangle (compressed walk: candidate hits re-test their leaf)
-    std::vector<float4> leafbox(RTG_QNODE ? std::max<size_t>((size_t)nt * 2, 2) : 2);
-    if (RTG_QNODE) {
-        for (uint32_t i = 0; i < nn; ++i) {
-            const int32_t* L = d->node_links + (size_t)i * 4;
-            if (L[0] >= 0) continue;
-            const float* b = d->node_bounds + (size_t)i * 6;
-            for (int t = L[2]; t < L[3]; ++t) {
-                leafbox[2 * (size_t)t] = make_float4(b[0], b[1], b[2], b[3]);
-                leafbox[2 * (size_t)t + 1] = make_float4(b[4], b[5], 0.0f, 0.0f);
-            }
+    std::vector<float4> leafbox(std::max<size_t>((size_t)nt * 2, 2));
+    for (uint32_t i = 0; i < nn; ++i) {
+        const int32_t* L = d->node_links + (size_t)i * 4;
+        if (L[0] >= 0) continue;
+        const float* b = d->node_bounds + (size_t)i * 6;
+        for (int t = L[2]; t < L[3]; ++t) {
+            leafbox[2 * (size_t)t] = make_float4(b[0], b[1], b[2], b[3]);
+            leafbox[2 * (size_t)t + 1] = make_float4(b[4], b[5], 0.0f, 0.0f);
         }
     }
     float scale = 0.0f;
@@ -1808,7 +1306,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         const DevTex& t = texinfo[mats[i].tex];
         if (t.w > 0xffff || t.h > 0xffff) { g_err = "texture larger than 65535 texels per side"; return RTG_ERR_ARG; }
         mats[i].tex = t.off;
-        mats[i].tex_wh = t.w | (t.h << 16);
+        mats[i].tex_wh = (int)((unsigned)t.w | ((unsigned)t.h << 16));
         mats[i].pad = 0;
         mats[i].texel0 = make_float4(texels[(size_t)t.off * 4], texels[(size_t)t.off * 4 + 1], texels[(size_t)t.off * 4 + 2], 0.0f);
     }
@@ -1833,14 +1331,9 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     }
     int rc;
     if ((rc = dev_upload(&h->d_nodes, nodes))) return rc;
-    if ((rc = dev_upload(&h->d_nodesw, nodesw))) return rc;
     if ((rc = dev_upload(&h->d_nodesq, nodesq))) return rc;
     if ((rc = dev_upload(&h->d_leafbox, leafbox))) return rc;
-    if (RTG_TRI48) {
-        if ((rc = dev_upload(&h->d_tris48, tris48))) return rc;
-    } else if ((rc = dev_upload(&h->d_tris, tris))) {
-        return rc;
-    }
+    if ((rc = dev_upload(&h->d_tris48, tris48))) return rc;
     if ((rc = dev_upload(&h->d_shade, shade))) return rc;
     if ((rc = dev_upload(&h->d_mats, mats))) return rc;
     if ((rc = dev_upload(&h->d_lights, lights))) return rc;
@@ -1849,7 +1342,6 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
 
     SceneView& s = h->sv;
     s.nodes = h->d_nodes;
-    s.tris = h->d_tris;
     s.tris48 = h->d_tris48;
     s.shade = h->d_shade;
     s.mats = h->d_mats;
@@ -1862,7 +1354,6 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     s.env_w = d->env_texture >= 0 ? texinfo[d->env_texture].w : 1;
     s.env_h = d->env_texture >= 0 ? texinfo[d->env_texture].h : 1;
     s.root_word = root_word;
-    s.nodesw = h->d_nodesw;
     s.nodesq = h->d_nodesq;
     s.leafbox = h->d_leafbox;
     s.root_wordw = root_wordw;
@@ -1887,10 +1378,6 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     HIPOK(hipMalloc((void**)&h->d_stats, 16 * sizeof(unsigned long long)));
     HIPOK(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
     for (auto& e : h->ev) HIPOK(hipEventCreate(&e));
-    for (auto& e : h->pev) HIPOK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPOK(hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking));
-    if (const char* e = std::getenv("RTG_PIPES")) h->pipes = std::atoi(e) >= 2 ? 2 : 1;
-    if (const char* e = std::getenv("RTG_STAGGER")) h->stagger = std::atoi(e);
 
     int occ = 0;
     HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false>, RTG_TB, 0));
@@ -1898,16 +1385,6 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     int occ3 = 0;
     HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_trace<true>, RTG_TB, 0));
     h->trace_blocks_count = h->n_cu * std::max(1, occ3);
-    int occp = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occp, k_trace_packet, RTG_TB, 0));
-    h->packet_blocks = h->n_cu * std::max(1, occp);
-    if (const char* e = std::getenv("RTG_PACKET")) h->packet = std::atoi(e);
-    if (const char* e = std::getenv("RTG_PIXEL_MAJOR")) h->pixel_major = std::atoi(e);
-    if (const char* e = std::getenv("RTG_FETCH8")) h->fetch8 = std::atoi(e);
-    int occs = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occs, k_shade<false>, RTG_TB, 0));
-    h->shade_blocks = h->n_cu * std::max(1, occs);
-    if (const char* e = std::getenv("RTG_SHADE_GRID")) h->shade_grid = std::atoi(e);
     return ensure_ovf(h);
 }
 
@@ -1927,17 +1404,13 @@ void rtg_destroy(rtg_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    if (h->stream2) (void)hipStreamSynchronize(h->stream2);
-    free_chunk(h, 0);
-    free_chunk(h, 1);
-    (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodesw); (void)hipFree(h->d_nodesq); (void)hipFree(h->d_leafbox); (void)hipFree(h->d_tris); (void)hipFree(h->d_tris48); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
+    free_chunk(h);
+    (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodesq); (void)hipFree(h->d_leafbox); (void)hipFree(h->d_tris48); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
     (void)hipFree(h->d_lights); (void)hipFree(h->d_texinfo); (void)hipFree(h->d_texels); (void)hipFree(h->d_film);
     (void)hipFree(h->d_pix); (void)hipFree(h->d_ovf); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
     for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
-    for (auto& e : h->pev) if (e) (void)hipEventDestroy(e);
     for (auto& e : h->kev) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
-    if (h->stream2) (void)hipStreamDestroy(h->stream2);
     delete h;
 }
 
@@ -1957,6 +1430,7 @@ int rtg_set_options(rtg_handle* h, int max_depth, int cull, uint32_t max_paths) 
     h->count = (cull >> 1) & 1;   // bit 1: counting kernels (node/triangle tests)
     h->timing = (cull >> 2) & 1;  // bit 2: per-launch timing events
     h->wide = ((cull >> 3) & 1) ? 0 : 1;  // bit 3: force the reference BVH2 walk
+    h->wavetime = RTG_DEBUG ? (cull >> 4) & 1 : 0;  // bit 4 (RTG_DEBUG builds): per-wave clocks
     if (max_paths) h->max_paths = max_paths;
     return RTG_OK;
 }
@@ -2037,24 +1511,17 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         size_t freeb = 0, totalb = 0;
         if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
             auto path_bytes = [](int pl) { return (size_t)152 + (size_t)16 * (size_t)pl; };
-            size_t held = 0;
-            for (int i = 0; i < 2; ++i) held += h->cap_P[i] * path_bytes(h->cap_maxb[i]);
-            const size_t budget = (freeb + held) / 2 / (h->pipes >= 2 ? 2 : 1);
+            const size_t held = h->cap_P * path_bytes(h->cap_maxb);
+            const size_t budget = (freeb + held) / 2;
             const size_t max_ns = budget / path_bytes(planes) / std::max<size_t>(1, h->npix);
             ns_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(ns_chunk, max_ns));
         }
     }
-    // Two chunk pipelines: the samples are split into (at least) two chunks that alternate between
-    // the caller's stream and stream2, so that one chunk's trace drain tails (a few hundred us per
-    // launch: the longest rays' dependent fetch chains) overlap the other chunk's work. The film
-    // fold stays in sample order: chunk c's k_accumulate waits for chunk c-1's.
-    const int pipes = (h->pipes >= 2 && n_samples >= 2) ? 2 : 1;
-    if (pipes == 2 && ns_chunk >= n_samples) ns_chunk = (n_samples + 1) / 2;
     // Keep the chunk buffers once they hold most of what the budget asks for: the free-memory
     // reading moves between calls, and growing a buffer of ~100 GB means a free and a new
-    // hipMalloc that took 5.5 s on C4 with 1G paths in flight (tools/c4_stall.sh).
+    // hipMalloc that took 5.5 s on C4 with 1G paths in flight.
     {
-        const uint32_t fit = h->cap_maxb[0] >= planes ? (uint32_t)(h->cap_P[0] / std::max(1u, h->npix)) : 0u;
+        const uint32_t fit = h->cap_maxb >= planes ? (uint32_t)(h->cap_P / std::max(1u, h->npix)) : 0u;
         if (fit >= 1 && ns_chunk > fit && (uint64_t)fit * 4 >= (uint64_t)ns_chunk * 3) ns_chunk = fit;
     }
     // equal chunks: 256 samples at <= 123 per chunk run as 86 + 85 + 85, not 123 + 123 + 10 (a thin
@@ -2064,42 +1531,27 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         ns_chunk = (n_samples + nchunks - 1) / nchunks;
     }
     const size_t P = (size_t)ns_chunk * h->npix;
-    for (int i = 0; i < pipes; ++i)
-        if ((rc = ensure_chunk(h, i, P, planes))) return rc;
+    if ((rc = ensure_chunk(h, P, planes))) return rc;
     if ((rc = ensure_ovf(h))) return rc;
     (void)hipGetLastError();  // drop any stale error left by other code on this thread
     HIPOK(hipEventRecord(h->ev[0], st));
-    if (pipes == 2) {  // stream2 starts after everything already queued on the caller's stream
-        HIPOK(hipEventRecord(h->pev[0], st));
-        HIPOK(hipStreamWaitEvent(h->stream2, h->pev[0], 0));
-    }
-    // packet walk for the camera rays (k_trace_packet): compressed wide tree available, its stack
-    // depth bound fits RTG_PSTACK, not counting (the counting pass measures the per-lane walk)
-    const bool use_packet = h->packet && !h->count && h->wide && h->usew && RTG_QNODE && !RTG_NODE48 && RTG_TRI48 &&
-                            h->wide_depth * RTG_WIDTH + 1 <= RTG_PSTACK;
-    std::vector<int> kinds;  // 0 extend, 1 shadow, 2 other (timing mode)
+    std::vector<int> kinds;  // 0 trace, 2 other (timing mode)
     size_t k = 0;
+    PathBufs& pb = h->pb;
     TraceIO io{};
     io.stats = h->d_stats;
     io.cull = h->cull;
     io.wide = h->wide;
-    // RTG_WAVETIME (diagnostic): per-wave clocks of chunk 0's trace launches, summarised on stderr
+    io.ovf = h->d_ovf;
+    // RTG_DEBUG builds with RTG_OPT_WAVETIME: per-wave clocks of chunk 0's trace launches, on stderr
     unsigned long long* d_wt = nullptr;
     const size_t wt_waves = (size_t)std::max(h->trace_blocks, h->trace_blocks_count) * (RTG_TB / 64);
-    if (std::getenv("RTG_WAVETIME")) {
+    if (RTG_DEBUG && h->wavetime) {
         HIPOK(hipMalloc((void**)&d_wt, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long)));
         HIPOK(hipMemsetAsync(d_wt, 0, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long), st));
     }
     uint32_t c = 0;
     for (uint32_t s0 = first; s0 < first + n_samples; s0 += ns_chunk, ++c) {
-        const int pi = pipes == 2 ? (int)(c & 1) : 0;
-        hipStream_t cs = pi ? h->stream2 : st;
-        PathBufs& pb = h->pb[pi];
-        io.ovf = h->d_ovf + (size_t)pi * (h->cap_ovf / 2);
-        // stagger: chunk 1 starts after chunk 0's generate (1) or first trace launch (2), so the
-        // two pipelines' drain tails fall at different times (0: both start together)
-        if (pipes == 2 && c == 1 && (h->stagger == 1 || h->stagger == 2))
-            HIPOK(hipStreamWaitEvent(cs, h->pev[1], 0));
         ChunkArgs a;
         a.pixlist = h->d_pix;
         a.npix = h->npix;
@@ -2109,31 +1561,29 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         a.seed = seed;
         a.max_depth = h->max_depth;
         a.mode = h->integrator;
-        a.pm = h->pixel_major;
         a.cam = h->cam;
-        a.lean = RTG_GEN_LEAN && !use_packet;
-        HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), cs));
-        timed_begin(h, cs, k);
-        hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, cs, a, pb);
+        a.lean = 1;
+        HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), st));
+        timed_begin(h, st, k);
+        hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, pb);
         LAUNCH_OK("k_generate");
-        timed_end(h, cs, k); kinds.push_back(2); ++k;
-        if (pipes == 2 && c == 0 && h->stagger == 1) HIPOK(hipEventRecord(h->pev[1], cs));
+        timed_end(h, st, k); kinds.push_back(2); ++k;
         // Trace launch L_b (b = 0..maxb) carries the extension rays of bounce b (from shade(b-1),
         // or generate) and the shadow rays of bounce b-1: one persistent launch, one drain tail.
         for (int b = 0; b <= maxb; ++b) {
             if (b > 0) {
-                timed_begin(h, cs, k);
-                const unsigned sgrid = h->shade_grid > 0 ? (unsigned)((a.P + (size_t)RTG_TB * h->shade_grid - 1) / ((size_t)RTG_TB * h->shade_grid))
-                                                         : (unsigned)h->shade_blocks;
+                // one 256-path tile per block (blocks past the live count exit at once)
+                timed_begin(h, st, k);
+                const unsigned sgrid = (unsigned)((a.P + RTG_TB - 1) / RTG_TB);
                 if (h->integrator == RTG_INTEGRATOR_PATH)
-                    hipLaunchKernelGGL(k_shade<false>, dim3(sgrid), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
+                    hipLaunchKernelGGL(k_shade<false>, dim3(sgrid), dim3(RTG_TB), 0, st, h->sv, a, pb, b - 1);
                 else
-                    hipLaunchKernelGGL(k_shade<true>, dim3(sgrid), dim3(RTG_TB), 0, cs, h->sv, a, pb, b - 1);
+                    hipLaunchKernelGGL(k_shade<true>, dim3(sgrid), dim3(RTG_TB), 0, st, h->sv, a, pb, b - 1);
                 LAUNCH_OK("k_shade");
-                timed_end(h, cs, k); kinds.push_back(2); ++k;
+                timed_end(h, st, k); kinds.push_back(2); ++k;
             }
-            io.queue = (a.lean && b == 0) ? nullptr : pb.q[b & 1];
-            io.ray_o = (a.lean && b == 0) ? nullptr : pb.ray_o;
+            io.queue = b == 0 ? nullptr : pb.q[b & 1];  // bounce 0: identity queue, camera origin
+            io.ray_o = b == 0 ? nullptr : pb.ray_o;
             io.cam_o = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f);
             io.ray_d = pb.ray_d;
             io.count = b < maxb ? &pb.ctr[b].n_ext : nullptr;
@@ -2146,48 +1596,25 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             io.contrib = b > 0 ? pb.contrib + (size_t)(b - 1) * a.P : nullptr;
             io.visible = nullptr;
             io.fetch = &pb.ctr[b].f_ext;
-            io.fetch8 = h->fetch8 ? pb.ctr[b].f8 : nullptr;
+            io.fetch8 = pb.ctr[b].f8;
             io.wtime = (d_wt && c == 0) ? d_wt + (size_t)b * wt_waves * 3 : nullptr;
-            timed_begin(h, cs, k);
-            if (b == 0 && use_packet) {
-                // camera rays: packet walk, then the per-lane walk for its leftover rays (zero
-                // direction components; usually none)
-                io.fetch = &pb.ctr[0].f_ext;
-                hipLaunchKernelGGL(k_trace_packet, dim3(h->packet_blocks), dim3(RTG_TB), 0, cs, h->sv, io, pb.shq,
-                                   &pb.ctr[0].pad0);
-                LAUNCH_OK("k_trace_packet");
-                TraceIO lo = io;
-                lo.queue = pb.shq;
-                lo.count = &pb.ctr[0].pad0;
-                lo.fetch = &pb.ctr[0].pad1;
-                lo.fetch8 = nullptr;
-                hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, cs, h->sv, lo);
-            } else if (h->count) {
-                hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, cs, h->sv, io);
-            } else {
-                hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, cs, h->sv, io);
-            }
+            timed_begin(h, st, k);
+            if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
+            else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
             LAUNCH_OK("k_trace");
-            timed_end(h, cs, k); kinds.push_back(0); ++k;
-            if (pipes == 2 && c == 0 && b == 0 && h->stagger == 2) HIPOK(hipEventRecord(h->pev[1], cs));
+            timed_end(h, st, k); kinds.push_back(0); ++k;
         }
-        hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, cs, pb.ctr, maxb, h->d_stats);
+        hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, st, pb.ctr, maxb, h->d_stats);
         LAUNCH_OK("k_tally");
-        if (pipes == 2 && c > 0) HIPOK(hipStreamWaitEvent(cs, h->pev[3], 0));  // fold order
-        timed_begin(h, cs, k);
-        if (a.pm && a.ns > 1)
-            hipLaunchKernelGGL(k_accumulate_pm, dim3((h->npix + RTG_TB / 64 - 1) / (RTG_TB / 64)), dim3(RTG_TB), 0, cs, a,
+        timed_begin(h, st, k);
+        if (a.ns > 1)
+            hipLaunchKernelGGL(k_accumulate_pm, dim3((h->npix + RTG_TB / 64 - 1) / (RTG_TB / 64)), dim3(RTG_TB), 0, st, a,
                                pb, h->d_film);
         else
-            hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, cs, a, pb, h->d_film);
+            hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, pb, h->d_film);
         LAUNCH_OK("k_accumulate");
-        timed_end(h, cs, k); kinds.push_back(2); ++k;
-        if (pipes == 2) HIPOK(hipEventRecord(h->pev[3], cs));
+        timed_end(h, st, k); kinds.push_back(2); ++k;
         h->stats.paths += a.P;
-    }
-    if (pipes == 2) {  // join: the caller's stream waits for stream2's chunks
-        HIPOK(hipEventRecord(h->pev[2], h->stream2));
-        HIPOK(hipStreamWaitEvent(st, h->pev[2], 0));
     }
     if (d_wt) {
         std::vector<unsigned long long> wt((size_t)(maxb + 1) * wt_waves * 3);
@@ -2227,7 +1654,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         for (size_t j = 0; j < kinds.size(); ++j) {
             float ms = 0;
             (void)hipEventElapsedTime(&ms, h->kev[2 * j], h->kev[2 * j + 1]);
-            (kinds[j] == 0 ? h->stats.extend_ms : kinds[j] == 1 ? h->stats.shadow_ms : h->stats.shade_ms) += ms;
+            (kinds[j] == 0 ? h->stats.extend_ms : h->stats.shade_ms) += ms;
             if (kinds[j] == 0) h->stats.extend_launches++;
         }
     }

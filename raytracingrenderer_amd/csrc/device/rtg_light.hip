@@ -540,7 +540,7 @@ int rtg_render_light(rtg_handle* h, uint32_t first, uint32_t n_frames, uint64_t 
     if ((uint64_t)first + n_frames > 65536u) { g_err = "frame index >= 65536 (PCG stream key)"; return RTG_ERR_ARG; }
     const size_t P = std::min<size_t>(npaths, h->max_paths);
     int rc;
-    if ((rc = ensure_chunk(h, 0, P, std::max(h->cap_maxb[0], 1)))) return rc;
+    if ((rc = ensure_chunk(h, P, std::max(h->cap_maxb, 1)))) return rc;
     if ((rc = ensure_ovf(h))) return rc;
     // records: at most one per path and vertex; grown on demand
     size_t cap = 4 * P + 1024;
@@ -549,7 +549,7 @@ int rtg_render_light(rtg_handle* h, uint32_t first, uint32_t n_frames, uint64_t 
     DALLOC(rn, 16);
     size_t tmp_bytes = 0;
     const DevProj cam = make_proj(h);
-    PathBufs& pb = h->pb[0];
+    PathBufs& pb = h->pb;
     for (uint32_t f = first; f < first + n_frames; ++f) {
         for (size_t base = 0; base < npaths; base += P) {
             LightArgs a{};
@@ -605,9 +605,9 @@ int rtg_render_instant_radiosity(rtg_handle* h, uint32_t first, uint32_t n_frame
     int rc;
     if ((rc = set_pixels(h, nullptr, 0))) return rc;
     const unsigned npix = h->npix;
-    if ((rc = ensure_chunk(h, 0, std::max<size_t>(npix, n_vpl), std::max(h->cap_maxb[0], 1)))) return rc;
+    if ((rc = ensure_chunk(h, std::max<size_t>(npix, n_vpl), std::max(h->cap_maxb, 1)))) return rc;
     if ((rc = ensure_ovf(h))) return rc;
-    PathBufs& pb = h->pb[0];
+    PathBufs& pb = h->pb;
     const DevProj cam = make_proj(h);
     size_t cap = 64 * (size_t)n_vpl + 1024;
     DevBuf vkey, vrec, rn, px, pn, pf, acc, vpl_d;

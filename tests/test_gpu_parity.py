@@ -81,11 +81,9 @@ def test_wide_walk_is_exact(cornell256, synth20k):
         assert np.array_equal(a.trace_visible(r), b.trace_visible(r))
 
 
-@pytest.mark.parametrize("rebuild", ["0", "1"])
-def test_wide_walk_tree_source(rebuild, synth20k, cornell256, monkeypatch):
-    """Wide nodes cut from the reference BVH2 (RTG_REBUILD=0) or from the own 3-axis SAH tree over
-    the reference leaves (RTG_REBUILD=1, the default): both return the BVH2 walk's bits."""
-    monkeypatch.setenv("RTG_REBUILD", rebuild)
+def test_wide_walk_over_own_tree_equals_bvh2_walk(synth20k, cornell256):
+    """Wide nodes cut from the own 3-axis SAH tree over the reference leaves return the reference
+    BVH2 walk's bits: films and 100k random closest-hit / any-hit queries per scene."""
     rng = np.random.default_rng(31)
     for s in (synth20k, cornell256):
         assert_bitexact(gpu_film(s, 2, wide=True), gpu_film(s, 2, wide=False), "bvh4 vs bvh2 film")
@@ -427,23 +425,14 @@ def test_instant_radiosity_matches_oracle(scene_name):
     assert_bitexact(film, ref, "instant radiosity " + scene_name)
 
 
-def test_packet_walk_is_exact(synth20k, cornell256, monkeypatch):
-    """The experimental packet walk for camera rays (RTG_PACKET=1, k_trace_packet) gives the same
-    films bit for bit."""
-    monkeypatch.setenv("RTG_PACKET", "1")
-    for s in (synth20k, cornell256):
-        assert_bitexact(gpu_film(s, 2), Oracle(s, 4, "rtm").render(2, seed=1234, threads=8)[0], "packet walk")
-
-
-def test_many_samples_per_chunk_and_path_order(monkeypatch):
-    """130 samples of every pixel in one chunk: pixel-major path ids fold the film in two passes of
-    64 samples (k_accumulate_pm) and must equal the oracle bit for bit; the sample-major order
-    (RTG_PIXEL_MAJOR=0, k_accumulate) gives the same film."""
+def test_many_samples_per_chunk_and_path_order():
+    """130 samples of every pixel in one chunk: pixel-major path ids fold the film in three passes
+    of up to 64 samples (k_accumulate_pm) and must equal the oracle bit for bit; one sample per
+    chunk (k_accumulate) gives the same film."""
     s = loadScene(os.path.join(SCENES, "cornell-box"), width=32, height=32)
     ref, _ = Oracle(s, 4, "rtm").render(130, seed=1234, threads=8)
-    assert_bitexact(gpu_film(s, 130), ref, "pixel-major 130 spp")
-    monkeypatch.setenv("RTG_PIXEL_MAJOR", "0")
-    assert_bitexact(gpu_film(s, 130), ref, "sample-major 130 spp")
+    assert_bitexact(gpu_film(s, 130), ref, "130 spp in one chunk")
+    assert_bitexact(gpu_film(s, 130, max_paths=32 * 32), ref, "one sample per chunk")
 
 
 def test_adaptive_render_many_frames_and_key_limit():
