@@ -9,7 +9,12 @@ the reduced film is bit-identical to a 1-GPU render). Total work is fixed as N g
 scaling). Scene generation, loading and BVH build happen before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+      N > 1 without torchrun: one process drives N GPUs through the native group (rtg_group_*:
+      one handle and host thread per device, ncclCommInitAll + ncclReduce of the film), the path an
+      RTBase C++ host takes. N must not exceed the visible devices (exit status 2 otherwise).
+  python bench.py --devices 0,0 [--verify-film]
+      the same group path over an explicit device list; repeats rehearse N ranks on one GPU
+  torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL via torch)
 """
 import argparse
 import json
@@ -67,9 +72,56 @@ def scene_dir(name):
     raise SystemExit("scene %s not found (run __graft_entry__.build() where /root/reference exists)" % name)
 
 
+class GroupRender:
+    """The native one-process group (RayTracerGroup: rtg_group_* in rtg_multi.hip) behind the calls
+    bench.py makes on a RayTracer: render = every rank renders its diagonal tile stripes on its own
+    device (one host thread each), then the RCCL film reduce into devices[0]; stats are summed over
+    the ranks."""
+
+    def __init__(self, scene, devices, max_depth, max_paths):
+        from raytracingrenderer_amd import RayTracerGroup
+        t0 = time.perf_counter()
+        self.g = RayTracerGroup(scene, devices=devices, max_depth=max_depth, seed=1234, max_paths=max_paths)
+        self.create_s = time.perf_counter() - t0
+        self.devices = list(devices)
+        self.reduce_ms = []
+        self.last_ranks = []
+
+    def set_options(self, flags):
+        self.g.set_options(flags=flags)
+
+    def clear(self):
+        self.g.clear()
+
+    def render(self, spp, tiles=None, first_sample=0):
+        self.g.render(spp, first_sample=first_sample)  # synchronous per rank
+        self.g.reduce()
+        self.reduce_ms.append(self.g.reduce_ms())
+
+    def synchronize(self):
+        pass  # group calls return when their devices are done
+
+    def stats(self):
+        self.last_ranks = self.g.rank_stats()
+        return {k: sum(r[k] for r in self.last_ranks) for k in self.last_ranks[0]}
+
+    def film(self):
+        return self.g.film()
+
+
+def visible_devices():
+    import ctypes as C
+    from raytracingrenderer_amd import _native as N
+    n = C.c_int(0)
+    N.rtg().rtg_device_count(C.byref(n))
+    return n.value
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--devices", default="",
+                   help="comma-separated device list for the native group path (repeats rehearse ranks)")
     p.add_argument("--config", default="C3", choices=sorted(CONFIGS),
                    help="BASELINE.json config; C3 is the headline metric, the others are side measurements")
     p.add_argument("--steps", type=int, default=3)
@@ -87,7 +139,7 @@ def parse():
                    help="diagnostic: render only rank 0's tiles of this many ranks, on one GPU, to see the "
                         "per-GPU rate at that world size (value is then this GPU's rate, not a job total)")
     p.add_argument("--verify-film", action="store_true",
-                   help="N>1: rank 0 re-renders every tile alone and checks the reduced film bit for bit")
+                   help="N>1: every tile re-rendered on one device, compared with the reduced film bit for bit")
     p.add_argument("--max-paths", type=int, default=0, help="paths per wavefront chunk (0 = library default)")
     a = p.parse_args()
     c = CONFIGS[a.config]
@@ -122,6 +174,17 @@ def main():
     from raytracingrenderer_amd import RayTracer, loadScene, write_synthetic_scene
     from raytracingrenderer_amd import _native as N
 
+    # one process, several GPUs: the native group (no torchrun)
+    group_devs = None
+    if world == 1 and (a.devices or a.gpus > 1):
+        nvis = visible_devices()
+        group_devs = [int(x) for x in a.devices.split(",")] if a.devices else list(range(a.gpus))
+        if (not a.devices and a.gpus > nvis) or any(d < 0 or d >= nvis for d in group_devs):
+            sys.stderr.write("bench.py: %s needs devices %s but %d HIP device(s) are visible; refusing to "
+                             "measure fewer GPUs than asked (--devices 0,0,... rehearses ranks on one GPU)\n"
+                             % ("--gpus %d" % a.gpus if not a.devices else "--devices " + a.devices, group_devs, nvis))
+            sys.exit(2)
+
     # ---- scene (outside the timed region)
     cfg = CONFIGS[a.config]
     t0 = time.time()
@@ -134,11 +197,15 @@ def main():
         scene = loadScene(work, width=a.width, height=a.height,
                           skip_missing=cfg.get("skip_missing", False), envmap=cfg.get("envmap"))
     setup_s = time.time() - t0
-    rt = RayTracer(scene, device=local, max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
     from raytracingrenderer_amd.distributed import reduce_film, tiles_for_rank
-    tiles = tiles_for_rank(a.width, a.height, rank, world)
-    if a.shard_of > 1 and world == 1:
-        tiles = tiles_for_rank(a.width, a.height, 0, a.shard_of)
+    if group_devs is not None:
+        rt = GroupRender(scene, group_devs, a.max_depth, a.max_paths)
+        tiles = None  # the group partitions the tiles itself (rtg_tiles_for_rank)
+    else:
+        rt = RayTracer(scene, device=local, max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
+        tiles = tiles_for_rank(a.width, a.height, rank, world)
+        if a.shard_of > 1 and world == 1:
+            tiles = tiles_for_rank(a.width, a.height, 0, a.shard_of)
 
     film_t = None
     if world > 1:
@@ -203,6 +270,14 @@ def main():
     rt.set_options(flags=base)
 
     film_check = None
+    if group_devs is not None and a.verify_film:
+        rt.clear()
+        rt.render(a.spp, first_sample=0)
+        reduced = rt.film()[0]
+        solo = RayTracer(scene, device=group_devs[0], max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
+        solo.render(a.spp, first_sample=0)
+        film_check = bool(np.array_equal(reduced.view(np.uint32), solo.film()[0].view(np.uint32)))
+        del solo
     if world > 1 and a.verify_film:
         step()  # a fresh reduced film
         barrier_sync()
@@ -215,6 +290,18 @@ def main():
         barrier_sync()
 
     local_kernel_ms = (extend_ms, shadow_ms, shade_ms)
+    group_info = None
+    if group_devs is not None:
+        r0 = rt.last_ranks[0] if rt.last_ranks else {}
+        local_kernel_ms = (r0.get("extend_ms", 0.0) * a.steps, 0.0, r0.get("shade_ms", 0.0) * a.steps)
+        prep_ms, up_ms = rt.g.setup_ms()
+        timed_reduce = rt.reduce_ms[a.warmup:a.warmup + a.steps]
+        group_info = {"devices": group_devs, "distinct_gpus": len(set(group_devs)), "uses_rccl": rt.g.uses_rccl,
+                      "setup_ms": {"create_total": round(rt.create_s * 1e3, 1), "host_build": round(prep_ms, 1),
+                                   "parallel_uploads": round(up_ms, 1)},
+                      "reduce_ms_per_step": round(float(np.mean(timed_reduce)), 3) if timed_reduce else None,
+                      "rank_kernel_ms_last_step": [{"trace": round(r["extend_ms"], 2), "shade": round(r["shade_ms"], 2),
+                                                    "render": round(r["render_ms"], 2)} for r in rt.last_ranks]}
     totals = np.array([ext_rays, shadow_rays, paths, extend_ms, extend_launches,
                        cs["node_visits"], cs["tri_tests"], cs["extension_rays"],
                        cw["node_visits"], cw["tri_tests"],
@@ -276,7 +363,7 @@ def main():
     # measured HBM traffic per launch (PMC, profiles/): only for the profiled workload (C3, 64 spp,
     # one rank); other configs, shards and N > 1 have other launch sizes and report null
     traffic = None
-    profiled = (a.config == "C3" and world == 1 and a.shard_of <= 1 and a.spp == 64 and a.tris == 1_000_000
+    profiled = (a.config == "C3" and world == 1 and group_devs is None and a.shard_of <= 1 and a.spp == 64 and a.tris == 1_000_000
                 and (a.width, a.height) == (1024, 1024) and a.max_depth == 4)
     if profiled and os.path.exists(PMC_SUMMARY):
         try:
@@ -285,7 +372,7 @@ def main():
             traffic = None
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and group_devs is None and not a.no_cpu_baseline:
         cpu = cpu_baseline(scene, a, work)
 
     if rank == 0:
@@ -294,7 +381,7 @@ def main():
                        if a.config == "C3" else "Mray/s (closest-hit + shadow rays), config %s" % a.config),
             "value": round(mrays, 2),
             "unit": "Mray/s",
-            "n_gpus": world,
+            "n_gpus": world if group_devs is None else len(group_devs),
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_step, 3),
@@ -312,7 +399,11 @@ def main():
                            a.config, "synth-1M" if cfg["scene"] is None else cfg["scene"] + ("_f" if cfg.get("skip_missing") else ""),
                            a.width, a.height, a.spp, a.max_depth),
                        "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
-                       "max_depth": a.max_depth, "parallelism": "tile-sharded x%d + RCCL film reduce" % world},
+                       "max_depth": a.max_depth,
+                       "parallelism": ("tile-sharded x%d + RCCL film reduce" % world if group_devs is None else
+                                       "tile-sharded x%d, one process (rtg_group: a handle and host thread per device) + "
+                                       "%s film reduce" % (len(group_devs), "RCCL ncclReduce" if rt.g.uses_rccl
+                                                           else "host-memory (repeated devices)"))},
             "roofline": {"bound": "dependent-random-record-fetches", "kernel": "k_trace (extension + shadow rays)",
                          "achieved": None if achieved_rec is None else round(achieved_rec, 1),
                          "peak": None if ceiling is None else round(ceiling["g_lane_steps_per_s"], 1),
@@ -369,6 +460,7 @@ def main():
                                          "generate_shade_accumulate": round(local_kernel_ms[2] / a.steps, 2)},
             "cpu_baseline": cpu,
             **({"film_reduce_bit_exact": film_check} if film_check is not None else {}),
+            **({"group": group_info} if group_info is not None else {}),
             "setup_s": round(setup_s, 2),
         }
         print(json.dumps(out), flush=True)

@@ -210,7 +210,11 @@ int  rtg_render_adaptive(rtg_handle* h, uint32_t first_sample, uint64_t seed, ui
  * (rtg_tiles_for_rank; the partition of raytracingrenderer_amd/distributed.py), one host thread and
  * one handle per device, and rtg_group_reduce sums the float films into devices[0] with one RCCL
  * ncclReduce (ncclCommInitAll, single process). The reduced film is bit-identical to a one-device
- * render. A device list with repeats (N ranks rehearsed on fewer GPUs) sums through host memory. */
+ * render. A device list with repeats (N ranks rehearsed on fewer GPUs) renders the ranks in turn and
+ * sums through host memory. The scene's device records are built on the host once and uploaded to
+ * the devices in parallel (rtg_group_setup_ms). A failed rtg_group_render leaves the group
+ * poisoned (other ranks already added their samples): rtg_group_reduce / film_read return
+ * RTG_ERR_ARG until rtg_group_clear. */
 typedef struct rtg_group rtg_group;
 int  rtg_tiles_for_rank(uint32_t width, uint32_t height, int rank, int world, uint32_t* tile_ids /* or NULL */,
                         uint32_t* n_tiles);
@@ -225,6 +229,7 @@ int  rtg_group_film_read(rtg_group* g, float* rgb_sum /* width*height*3 */, uint
 int  rtg_group_clear(rtg_group* g);
 double rtg_group_reduce_ms(rtg_group* g);  /* device time of the last reduce */
 int  rtg_group_uses_rccl(rtg_group* g);    /* 1: RCCL communicator, 0: host-memory sum (repeated devices) */
+int  rtg_group_setup_ms(rtg_group* g, double* prepare_ms, double* upload_ms);  /* host build, parallel uploads */
 
 /* Film access: the unnormalised sum (Film::film) and the sample count (Film::SPP). */
 int  rtg_film_read(rtg_handle* h, float* rgb_sum /* width*height*3 */, uint32_t* spp);

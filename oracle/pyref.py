@@ -28,6 +28,8 @@ def lib(flavour="libm"):
                      "ref_camera_project", "ref_light_emit"):
             getattr(L, name).restype = None
         L.ref_bsdf_sample.restype = None
+        L.ref_rtg_desc.restype = vp
+        L.ref_rtg_desc.argtypes = [vp]
         L.ref_save_hdr.restype = C.c_int
         L.ref_load_texture.restype = C.c_int
         _libs[flavour] = L
@@ -62,6 +64,11 @@ class RefScene:
         L.ref_render_mode(self.h, first, n_samples, seed, max_depth, threads, film.ctypes.data, counts.ctypes.data,
                           mode)
         return film, counts
+
+    def rtg_desc(self):
+        """Pointer to the rtg_scene_desc built by integration/rtg_rtbase.h (rtg_flatten_scene) from
+        this reference Scene; valid while this object lives."""
+        return self.L.ref_rtg_desc(C.c_void_p(self.h))
 
     def export(self):
         n, m = self.ntri, self.nnode

@@ -17,6 +17,7 @@
 // film-level pin of the C oracle and the "reference" CPU baseline of bench.py.
 #include "GEMLoader.h"
 #include "Scene.h"
+#include "../../integration/rtg_rtbase.h"  // the reference-side binding
 
 #include <sys/stat.h>
 
@@ -326,6 +327,7 @@ struct RefScene {
     std::vector<int> mat_kind, mat_two_sided, mat_tex;
     std::vector<float> mat_ior;             // int, ext
     int env_tex = -1;
+    RtgSceneBinding* binding = nullptr;     // rtg_flatten_scene's output (built on first use)
 };
 
 // SceneLoader.h:104-235 restated on the reference classes.
@@ -531,6 +533,17 @@ void ref_export(void* h, float* pos, float* nrm, float* uv, uint32_t* mat, float
         mat_f[i * 5 + 3] = s->materials[i]->emission.g;
         mat_f[i * 5 + 4] = s->materials[i]->emission.b;
     }
+}
+
+// The reference-side binding (integration/rtg_rtbase.h) applied to this Scene: the rtg_scene_desc
+// an RTBase host hands to rtg_create. Owned by the scene handle.
+const rtg_scene_desc* ref_rtg_desc(void* h) {
+    RefScene* rs = (RefScene*)h;
+    if (!rs->binding) {
+        rs->binding = new RtgSceneBinding();
+        rtg_flatten_scene(rs->scene, *rs->binding);
+    }
+    return &rs->binding->desc;
 }
 
 void ref_texture_size(void* h, int i, int* wh) {

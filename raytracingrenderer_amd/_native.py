@@ -107,6 +107,7 @@ RTG_EXPORTS = [
     ("rtg_group_clear", C.c_int, [C.c_void_p]),
     ("rtg_group_reduce_ms", C.c_double, [C.c_void_p]),
     ("rtg_group_uses_rccl", C.c_int, [C.c_void_p]),
+    ("rtg_group_setup_ms", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
 ]
 
 RTH_EXPORTS = [

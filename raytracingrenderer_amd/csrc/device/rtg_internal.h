@@ -183,7 +183,31 @@ struct rtg_handle {
 };
 
 
+// The device records of a scene, built on the host from an rtg_scene_desc (prepare_scene) and
+// uploaded per device (upload_scene); rtg_create does both, a group prepares once.
+struct HostScene {
+    std::vector<DevNode> nodes;
+    std::vector<DevNodeQ> nodesq;
+    std::vector<float4> leafbox;
+    std::vector<DevTri48> tris48;
+    std::vector<DevShade> shade;
+    std::vector<DevMat> mats;
+    std::vector<DevLight> lights;
+    std::vector<DevTex> texinfo;
+    std::vector<float> texels;
+    int n_lights = 0, env_tex = -1, env_off = 0, env_w = 1, env_h = 1;
+    int root_word = RTG_EXIT, root_wordw = RTG_EXIT;
+    bool usew = false, rebuilt = false;
+    uint32_t bvh_depth = 0, wide_depth = 0;
+    float root_box[6] = {0, 0, 0, 0, 0, 0};
+    float cull_scale = 0.0f;
+    DevCamera cam{};
+    rtg_camera_proj proj{};
+};
+
 // rtg_kernels.hip
+int prepare_scene(const rtg_scene_desc* d, HostScene& hs);
+int upload_scene(int device, const HostScene& hs, rtg_handle* h);
 int ensure_ovf(rtg_handle* h);
 int set_pixels(rtg_handle* h, const uint32_t* tiles, uint32_t n_tiles);
 int ensure_chunk(rtg_handle* h, size_t P, int maxb);

@@ -1085,23 +1085,15 @@ int rtg_device_count(int* count) {
     return RTG_OK;
 }
 
-static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
-        g_err = "no HIP device available";
-        return RTG_ERR_NO_DEVICE;
-    }
-    if (device < 0 || device >= ndev) { g_err = "bad device index"; return RTG_ERR_ARG; }
+}  // extern "C"
+
+// The host half of rtg_create: the descriptor (the flattened reference Scene) turned into the device
+// records. No HIP calls: a group builds this once and uploads it to every device in parallel.
+int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
     if (d->n_lights == 0) {
         g_err = "scene has no lights (RTBase's Scene::sampleLight indexes an empty list: Scene.h:137-138)";
         return RTG_ERR_NO_LIGHTS;
     }
-    h->device = device;
-    HIPOK(hipSetDevice(device));
-    HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-    hipDeviceProp_t prop;
-    HIPOK(hipGetDeviceProperties(&prop, device));
-    h->n_cu = prop.multiProcessorCount;
     const uint32_t nt = d->n_tris;
 
     // ---- triangles: Triangle::init (Geometry.h:72-83) + gNormal (:127-130)
@@ -1173,7 +1165,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             st.push_back({L[0], dep + 1});
         }
     }
-    h->bvh_depth = depth;
+    hs.bvh_depth = depth;
     int root_word = RTG_EXIT;
     if (nt > 0) {
         if (!word(0, root_word)) { g_err = "bad BVH root"; return RTG_ERR_ARG; }
@@ -1213,7 +1205,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
             out = ~(L[2] * RTG_LEAF_SPAN + (cnt - 1));
             return true;
         };
-        h->rebuilt = rebuilt;
+        hs.rebuilt = rebuilt;
         auto internal = [&](int i) { return LK[(size_t)i * 4] >= 0; };
         auto area = [&](int i) {
             const float* b = BD + (size_t)i * 6;
@@ -1241,7 +1233,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         while (!work.empty()) {
             auto [n2, nw, lvl] = work.back();
             work.pop_back();
-            h->wide_depth = std::max(h->wide_depth, (uint32_t)lvl);
+            hs.wide_depth = std::max(hs.wide_depth, (uint32_t)lvl);
             const std::vector<int> slots = cut(n2);
             int32_t wq[4] = {RTG_EXIT, RTG_EXIT, RTG_EXIT, RTG_EXIT};
             for (int k = 0; k < (int)slots.size(); ++k) {
@@ -1261,7 +1253,7 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     for (int k = 0; k < 6; ++k)
         if (std::isfinite(d->node_bounds[k])) cull_scale = std::max(cull_scale, std::fabs(d->node_bounds[k]));
     // the compressed walk's rounding margin is stated relative to the scene scale (k_trace)
-    h->usew = finite && qok && nt > 0 && cull_scale >= 0x1p-60f && cull_scale <= 0x1p60f;
+    hs.usew = finite && qok && nt > 0 && cull_scale >= 0x1p-60f && cull_scale <= 0x1p60f;
     // exact leaf boxes per triangle (compressed walk: candidate hits re-test their leaf)
     std::vector<float4> leafbox(std::max<size_t>((size_t)nt * 2, 2));
     for (uint32_t i = 0; i < nn; ++i) {
@@ -1329,16 +1321,64 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
         L.gn = make_float4(tri_gn[li * 3], tri_gn[li * 3 + 1], tri_gn[li * 3 + 2], 0.0f);
         L.em = make_float4(em[0], em[1], em[2], 0.0f);
     }
+    if (d->camera.width < 1.0f || d->camera.height < 1.0f) { g_err = "bad film size"; return RTG_ERR_ARG; }
+    hs.nodes = std::move(nodes);
+    hs.nodesq = std::move(nodesq);
+    hs.leafbox = std::move(leafbox);
+    hs.tris48 = std::move(tris48);
+    hs.shade = std::move(shade);
+    hs.mats = std::move(mats);
+    hs.lights = std::move(lights);
+    hs.texinfo = std::move(texinfo);
+    hs.texels = std::move(texels);
+    hs.n_lights = (int)d->n_lights;
+    hs.env_tex = d->env_texture;
+    hs.env_off = d->env_texture >= 0 ? hs.texinfo[d->env_texture].off : 0;
+    hs.env_w = d->env_texture >= 0 ? hs.texinfo[d->env_texture].w : 1;
+    hs.env_h = d->env_texture >= 0 ? hs.texinfo[d->env_texture].h : 1;
+    hs.root_word = root_word;
+    hs.root_wordw = root_wordw;
+    for (int k = 0; k < 6; ++k) hs.root_box[k] = d->node_bounds[k];
+    hs.cull_scale = scale;
+    std::memcpy(hs.cam.ip, d->camera.inv_proj, sizeof(hs.cam.ip));
+    std::memcpy(hs.cam.cm, d->camera.camera, sizeof(hs.cam.cm));
+    hs.cam.ox = d->camera.origin[0];
+    hs.cam.oy = d->camera.origin[1];
+    hs.cam.oz = d->camera.origin[2];
+    hs.cam.width = d->camera.width;
+    hs.cam.height = d->camera.height;
+    hs.proj = d->projection;
+    return RTG_OK;
+}
+
+// The device half: upload the prepared records to `device`, allocate the film, size the launches.
+int upload_scene(int device, const HostScene& hs, rtg_handle* h) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        g_err = "no HIP device available";
+        return RTG_ERR_NO_DEVICE;
+    }
+    if (device < 0 || device >= ndev) { g_err = "bad device index"; return RTG_ERR_ARG; }
+    h->device = device;
+    HIPOK(hipSetDevice(device));
+    HIPOK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    HIPOK(hipGetDeviceProperties(&prop, device));
+    h->n_cu = prop.multiProcessorCount;
+    h->bvh_depth = hs.bvh_depth;
+    h->wide_depth = hs.wide_depth;
+    h->rebuilt = hs.rebuilt;
+    h->usew = hs.usew;
     int rc;
-    if ((rc = dev_upload(&h->d_nodes, nodes))) return rc;
-    if ((rc = dev_upload(&h->d_nodesq, nodesq))) return rc;
-    if ((rc = dev_upload(&h->d_leafbox, leafbox))) return rc;
-    if ((rc = dev_upload(&h->d_tris48, tris48))) return rc;
-    if ((rc = dev_upload(&h->d_shade, shade))) return rc;
-    if ((rc = dev_upload(&h->d_mats, mats))) return rc;
-    if ((rc = dev_upload(&h->d_lights, lights))) return rc;
-    if ((rc = dev_upload(&h->d_texinfo, texinfo))) return rc;
-    if ((rc = dev_upload(&h->d_texels, texels))) return rc;
+    if ((rc = dev_upload(&h->d_nodes, hs.nodes))) return rc;
+    if ((rc = dev_upload(&h->d_nodesq, hs.nodesq))) return rc;
+    if ((rc = dev_upload(&h->d_leafbox, hs.leafbox))) return rc;
+    if ((rc = dev_upload(&h->d_tris48, hs.tris48))) return rc;
+    if ((rc = dev_upload(&h->d_shade, hs.shade))) return rc;
+    if ((rc = dev_upload(&h->d_mats, hs.mats))) return rc;
+    if ((rc = dev_upload(&h->d_lights, hs.lights))) return rc;
+    if ((rc = dev_upload(&h->d_texinfo, hs.texinfo))) return rc;
+    if ((rc = dev_upload(&h->d_texels, hs.texels))) return rc;
 
     SceneView& s = h->sv;
     s.nodes = h->d_nodes;
@@ -1348,30 +1388,22 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     s.lights = h->d_lights;
     s.texinfo = h->d_texinfo;
     s.texels = (const float4*)h->d_texels;
-    s.n_lights = (int)d->n_lights;
-    s.env_tex = d->env_texture;
-    s.env_off = d->env_texture >= 0 ? texinfo[d->env_texture].off : 0;
-    s.env_w = d->env_texture >= 0 ? texinfo[d->env_texture].w : 1;
-    s.env_h = d->env_texture >= 0 ? texinfo[d->env_texture].h : 1;
-    s.root_word = root_word;
+    s.n_lights = hs.n_lights;
+    s.env_tex = hs.env_tex;
+    s.env_off = hs.env_off;
+    s.env_w = hs.env_w;
+    s.env_h = hs.env_h;
+    s.root_word = hs.root_word;
     s.nodesq = h->d_nodesq;
     s.leafbox = h->d_leafbox;
-    s.root_wordw = root_wordw;
-    s.usew = h->usew ? 1 : 0;
-    for (int k = 0; k < 6; ++k) s.root_box[k] = d->node_bounds[k];
-    s.cull_scale = scale;
-
-    std::memcpy(h->cam.ip, d->camera.inv_proj, sizeof(h->cam.ip));
-    std::memcpy(h->cam.cm, d->camera.camera, sizeof(h->cam.cm));
-    h->cam.ox = d->camera.origin[0];
-    h->cam.oy = d->camera.origin[1];
-    h->cam.oz = d->camera.origin[2];
-    h->proj = d->projection;
-    h->cam.width = d->camera.width;
-    h->cam.height = d->camera.height;
-    h->W = (int)d->camera.width;
-    h->H = (int)d->camera.height;
-    if (h->W <= 0 || h->H <= 0) { g_err = "bad film size"; return RTG_ERR_ARG; }
+    s.root_wordw = hs.root_wordw;
+    s.usew = hs.usew ? 1 : 0;
+    for (int k = 0; k < 6; ++k) s.root_box[k] = hs.root_box[k];
+    s.cull_scale = hs.cull_scale;
+    h->cam = hs.cam;
+    h->proj = hs.proj;
+    h->W = (int)hs.cam.width;
+    h->H = (int)hs.cam.height;
     HIPOK(hipMalloc((void**)&h->d_film, (size_t)h->W * h->H * 3 * sizeof(float)));
     HIPOK(hipMemset(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float)));
     HIPOK(hipMalloc((void**)&h->d_qctr, 4 * sizeof(unsigned)));
@@ -1388,10 +1420,14 @@ static int create_impl(int device, const rtg_scene_desc* d, rtg_handle* h) {
     return ensure_ovf(h);
 }
 
+extern "C" {
+
 int rtg_create(int device, const rtg_scene_desc* desc, rtg_handle** out) {
     if (!desc || !out) { g_err = "rtg_create: null argument"; return RTG_ERR_ARG; }
     rtg_handle* h = new rtg_handle();
-    int rc = create_impl(device, desc, h);
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc == RTG_OK) rc = upload_scene(device, hs, h);
     if (rc != RTG_OK) {
         rtg_destroy(h);
         return rc;

@@ -10,7 +10,15 @@
 // bit-identical to a one-GPU render, whatever the reduction order.
 //
 // A device list that repeats a device (rehearsing N ranks on one GPU) cannot form an RCCL
-// communicator; the films are then summed through host memory in rank order (same bits).
+// communicator; the ranks then render one after another (concurrent handles on one GPU would each
+// size their path state from the same free-memory reading) and the films are summed through host
+// memory in rank order (same bits).
+//
+// Setup: the scene's device records are built once on the host (prepare_scene: triangle records,
+// the wide tree over the reference leaves, leaf boxes, materials, textures) and uploaded to every
+// device by its own thread (upload_scene), so an 8-GPU group costs one host build, not eight.
+// A rank that fails a render poisons the group: the other ranks' films already hold the samples,
+// so reduce / film_read refuse until rtg_group_clear.
 //
 // RCCL is opened with dlopen when a group first needs a communicator (not linked into librtg):
 // a process that also loads PyTorch gets PyTorch's bundled RCCL (same soname) instead of a second
@@ -22,6 +30,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -81,7 +90,10 @@ struct rtg_group {
     uint32_t W = 0, H = 0;
     uint32_t reduced_spp = 0;
     bool reduced = false;
+    bool distinct = true;                      // every rank on its own device (RCCL, concurrent ranks)
+    bool poisoned = false;                     // a rank failed a render: films hold partial samples
     double reduce_ms = 0.0;
+    double prepare_ms = 0.0, upload_ms = 0.0;  // group setup: host build once, parallel uploads
 };
 
 extern "C" {
@@ -119,18 +131,45 @@ int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* de
         return RTG_ERR_ARG;
     }
     *out = nullptr;
+    using clk = std::chrono::steady_clock;
+    auto t0 = clk::now();
+    HostScene hs;
+    int rc = prepare_scene(desc, hs);
+    if (rc) return rc;
+    auto t1 = clk::now();
     rtg_group* g = new rtg_group();
     g->devices.assign(devices, devices + n_devices);
     g->W = desc->camera.width;
     g->H = desc->camera.height;
-    for (int r = 0; r < n_devices; ++r) {
-        rtg_handle* h = nullptr;
-        const int rc = rtg_create(devices[r], desc, &h);
-        if (rc) {
+    g->prepare_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    g->h.assign(n_devices, nullptr);
+    std::vector<int> rcs(n_devices, RTG_OK);
+    std::vector<std::string> errs(n_devices);
+    auto up = [&](int r) {
+        rtg_handle* h = new rtg_handle();
+        rcs[r] = upload_scene(devices[r], hs, h);
+        if (rcs[r]) {
+            errs[r] = g_err;  // thread-local
+            rtg_destroy(h);
+            return;
+        }
+        g->h[r] = h;
+    };
+    {
+        std::vector<std::thread> pool;
+        for (int r = 0; r < n_devices; ++r) pool.emplace_back(up, r);
+        for (auto& t : pool) t.join();
+    }
+    g->upload_ms = std::chrono::duration<double, std::milli>(clk::now() - t1).count();
+    for (int r = 0; r < n_devices; ++r)
+        if (rcs[r]) {
+            rc = rcs[r];
+            g_err = "rank " + std::to_string(r) + ": " + errs[r];
+            g->h.erase(std::remove(g->h.begin(), g->h.end(), nullptr), g->h.end());
             rtg_group_destroy(g);
             return rc;
         }
-        g->h.push_back(h);
+    for (int r = 0; r < n_devices; ++r) {
         uint32_t n = 0;
         rtg_tiles_for_rank(g->W, g->H, r, n_devices, nullptr, &n);
         g->tiles.emplace_back(n);
@@ -138,8 +177,8 @@ int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* de
     }
     std::vector<int> sorted(g->devices);
     std::sort(sorted.begin(), sorted.end());
-    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    if (distinct) {
+    g->distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (g->distinct) {
         if (!load_rccl()) {
             rtg_group_destroy(g);
             return RTG_ERR_HIP;
@@ -160,6 +199,13 @@ int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* de
         return RTG_ERR_HIP;
     }
     *out = g;
+    return RTG_OK;
+}
+
+int rtg_group_setup_ms(rtg_group* g, double* prepare_ms, double* upload_ms) {
+    if (!g) return RTG_ERR_ARG;
+    if (prepare_ms) *prepare_ms = g->prepare_ms;
+    if (upload_ms) *upload_ms = g->upload_ms;
     return RTG_OK;
 }
 
@@ -189,8 +235,8 @@ int rtg_group_render(rtg_group* g, uint32_t first_sample, uint32_t n_samples, ui
         rc[r] = rtg_render(g->h[r], first_sample, n_samples, seed, t.data(), (uint32_t)t.size());
         if (rc[r]) err[r] = rtg_last_error();  // g_err is thread-local
     };
-    if (n == 1) {
-        run(0);
+    if (n == 1 || !g->distinct) {
+        for (size_t r = 0; r < n; ++r) run(r);  // one device: ranks in turn
     } else {
         std::vector<std::thread> pool;
         for (size_t r = 0; r < n; ++r) pool.emplace_back(run, r);
@@ -199,7 +245,8 @@ int rtg_group_render(rtg_group* g, uint32_t first_sample, uint32_t n_samples, ui
     g->reduced = false;
     for (size_t r = 0; r < n; ++r)
         if (rc[r]) {
-            g_err = "rank " + std::to_string(r) + ": " + err[r];
+            g->poisoned = true;
+            g_err = "rank " + std::to_string(r) + ": " + err[r] + " (group films now partial: rtg_group_clear)";
             return rc[r];
         }
     return RTG_OK;
@@ -207,6 +254,10 @@ int rtg_group_render(rtg_group* g, uint32_t first_sample, uint32_t n_samples, ui
 
 int rtg_group_reduce(rtg_group* g) {
     if (!g) return RTG_ERR_ARG;
+    if (g->poisoned) {
+        g_err = "rtg_group_reduce: a rank failed its last render; the films are partial until rtg_group_clear";
+        return RTG_ERR_ARG;
+    }
     const size_t n = g->h.size();
     const size_t count = (size_t)g->W * g->H * 3;
     EventPair ev;
@@ -279,6 +330,7 @@ int rtg_group_clear(rtg_group* g) {
         if (rc) return rc;
     }
     g->reduced = false;
+    g->poisoned = false;
     return RTG_OK;
 }
 

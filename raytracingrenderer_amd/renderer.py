@@ -309,8 +309,8 @@ class RayTracerGroup:
     tiles with (tile_x + tile_y) % N == r on devices[r] (one host thread per device), and film()
     sums the films into devices[0] with one RCCL reduce. The result is bit-identical to a one-device
     render (RayTracer::pathTracerTileBased's tile pool, Renderer.h:836-853, spread over devices).
-    A device list with repeats rehearses N ranks on fewer GPUs (the sum then goes through host
-    memory)."""
+    A device list with repeats rehearses N ranks on fewer GPUs (the ranks then render in turn and
+    the sum goes through host memory)."""
 
     def __init__(self, scene, devices=(0,), max_depth=RayTracer.MAX_DEPTH, seed=1234, cull=True, max_paths=0):
         self.scene = scene
@@ -323,9 +323,38 @@ class RayTracerGroup:
         _check(self._lib.rtg_group_create(N.ptr(dev, C.c_int32), len(dev), scene.desc_ptr, C.byref(g)),
                self._lib.rtg_last_error)
         self._g = g
-        _check(self._lib.rtg_group_set_options(g, max_depth, N.RTG_OPT_CULL if cull else 0, max_paths),
-               self._lib.rtg_last_error)
+        self.max_depth = max_depth
+        self.flags = N.RTG_OPT_CULL if cull else 0
+        _check(self._lib.rtg_group_set_options(g, max_depth, self.flags, max_paths), self._lib.rtg_last_error)
         self._spp = 0
+
+    def set_options(self, max_depth=None, flags=None, max_paths=0):
+        if max_depth is not None:
+            self.max_depth = max_depth
+        if flags is not None:
+            self.flags = flags
+        _check(self._lib.rtg_group_set_options(self._g, self.max_depth, self.flags, max_paths),
+               self._lib.rtg_last_error)
+
+    def setup_ms(self):
+        """(host build of the device records, parallel uploads) of rtg_group_create, in ms."""
+        a, b = C.c_double(), C.c_double()
+        _check(self._lib.rtg_group_setup_ms(self._g, C.byref(a), C.byref(b)), self._lib.rtg_last_error)
+        return a.value, b.value
+
+    def reduce(self):
+        """The RCCL film reduce into devices[0] (host sum for repeated devices); synchronous."""
+        _check(self._lib.rtg_group_reduce(self._g), self._lib.rtg_last_error)
+
+    def rank_stats(self):
+        """rtg_get_stats of every rank's handle (rays, kernel ms, counting-pass counters)."""
+        out = []
+        for r in range(len(self.devices)):
+            h = self._lib.rtg_group_handle(self._g, r)
+            st = N.rtg_stats()
+            _check(self._lib.rtg_get_stats(h, C.byref(st)), self._lib.rtg_last_error)
+            out.append({k: getattr(st, k) for k, _ in N.rtg_stats._fields_})
+        return out
 
     def __del__(self):
         g, self._g = getattr(self, "_g", None), None

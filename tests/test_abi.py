@@ -42,3 +42,12 @@ def test_no_gpu_fails_loudly():
     s = loadScene(os.path.join(SCENES, "cornell-box"), width=32, height=32)
     with pytest.raises(NativeError):
         RayTracer(s)
+
+
+def test_integration_doc_embeds_the_compiled_binding():
+    """INTEGRATION.md §2 shows integration/rtg_rtbase.h byte for byte (the header that
+    oracle/ref/Makefile compiles against the reference and the GPU tests render through)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    hdr = open(os.path.join(root, "integration", "rtg_rtbase.h")).read()
+    assert "```cpp\n" + hdr + "```" in doc

@@ -169,3 +169,81 @@ def test_cli_multi_gpu_output_equals_single(tmp_path, opt):
     assert r2.returncode == 0, r2.stderr
     assert ("RCCL" in r2.stdout) == (opt[0] == "-gpus")
     assert (tmp_path / "one" / "result_4.hdr").read_bytes() == (tmp_path / "multi" / "result_4.hdr").read_bytes()
+
+
+def _visible_gpus():
+    from conftest import has_gpu
+    if not has_gpu():
+        return 0
+    import ctypes as C
+    from raytracingrenderer_amd import _native as N
+    n = C.c_int(0)
+    N.rtg().rtg_device_count(C.byref(n))
+    return n.value
+
+
+@pytest.mark.gpu
+def test_group_over_distinct_devices_equals_one_device():
+    """rtg_group over two distinct GPUs (ncclCommInitAll over devices 0 and 1, a real 2-rank
+    ncclReduce over xGMI): the reduced film equals one device's render, bit for bit. Needs >= 2
+    visible GPUs (skipped on a one-GPU box; run on a node with several)."""
+    if _visible_gpus() < 2:
+        pytest.skip("needs >= 2 visible GPUs for a distinct-device RCCL group")
+    from raytracingrenderer_amd import RayTracer, RayTracerGroup, loadScene
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=160, height=96)
+    one = RayTracer(s, seed=17)
+    one.render(3, first_sample=0)
+    g = RayTracerGroup(s, devices=[0, 1], seed=17)
+    assert g.uses_rccl
+    g.render(3, first_sample=0)
+    assert np.array_equal(g.film()[0].view(np.uint32), one.film()[0].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_failed_group_render_poisons_until_clear():
+    """A rank that fails a render leaves the group's films partial: reduce / film_read refuse until
+    rtg_group_clear, after which the group renders the one-device film again."""
+    from raytracingrenderer_amd import RayTracer, RayTracerGroup, loadScene
+    from raytracingrenderer_amd.renderer import NativeError
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=64, height=64)
+    g = RayTracerGroup(s, devices=[0, 0], seed=3)
+    g.render(1, first_sample=0)
+    with pytest.raises(NativeError):
+        g.render(10, first_sample=65530)  # past the PCG key: every rank refuses
+    with pytest.raises(NativeError):
+        g.film()
+    g.clear()
+    g.render(2, first_sample=0)
+    one = RayTracer(s, seed=3)
+    one.render(2, first_sample=0)
+    assert np.array_equal(g.film()[0].view(np.uint32), one.film()[0].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_bench_native_group_rehearsal_is_bit_exact():
+    """bench.py --devices 0,0 (the native group path of --gpus N, two ranks rehearsed on one GPU)
+    reports n_gpus 2 and a reduced film equal to the one-device render."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--devices", "0,0", "--verify-film",
+                        "--config", "C2", "--width", "256", "--height", "192", "--spp", "4", "--steps", "1",
+                        "--warmup", "1", "--no-cpu-baseline"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["group"]["distinct_gpus"] == 1 and d["film_reduce_bit_exact"] is True
+    assert len(d["group"]["rank_kernel_ms_last_step"]) == 2
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """CPU: bench.py --gpus N with fewer visible HIP devices exits non-zero instead of silently
+    measuring one GPU (this container has none; a one-GPU box has one)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = _visible_gpus() + 1
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(max(n, 2)), "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "refusing" in r.stderr

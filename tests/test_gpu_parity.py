@@ -593,3 +593,35 @@ def test_count_mode_counters_are_consistent(synth20k, cornell256):
         tris = s["tri_tests"] + s["shadow_tri_tests"]
         assert 0 < s["leafbox_tests"] <= s["tri_tail_loads"] <= tris, s
         assert s["node_lane_steps"] > 0 and s["extension_rays"] > 0, s
+
+
+@pytest.mark.parametrize("case", ["cornell-mat", "bathroom", "coffee+GI"])
+def test_reference_side_binding_renders_reference_film(case):
+    """The drop-in from the reference side: RTBase's own loader builds the Scene (oracle/_ref, the
+    reference headers), integration/rtg_rtbase.h flattens it (the code INTEGRATION.md §2 shows),
+    rtg_create uploads it and rtg_render renders; the film equals RayTracer::pathTrace on the same
+    reference classes with glibc math (libref.so's ref_render), bit for bit."""
+    from oracle import pyref
+    if not pyref.available():
+        pytest.fail("oracle/_ref (libref.so) missing: build it where /root/reference exists")
+    path, kw, depth, spp, seed = {
+        "cornell-mat": (os.path.join(SCENES, "cornell-mat"), dict(width=80, height=60), 8, 3, 21),
+        "bathroom": (staged("bathroom"), dict(width=96, height=54, skip_missing=True), 16, 2, 22),
+        "coffee+GI": (staged("coffee"), dict(width=80, height=100, skip_missing=True, envmap="GI.hdr"), 4, 3, 23),
+    }[case]
+    r = pyref.RefScene(path, kw["width"], kw["height"], kw.get("skip_missing", False), kw.get("envmap"),
+                       flavour="libm")
+    ref, _ = r.render(spp, seed=seed, max_depth=depth, threads=8)
+    L = N.rtg()
+    h = C.c_void_p()
+    assert L.rtg_create(0, C.cast(r.rtg_desc(), C.POINTER(N.rtg_scene_desc)), C.byref(h)) == 0, L.rtg_last_error()
+    try:
+        assert L.rtg_set_options(h, depth, N.RTG_OPT_CULL, 0) == 0
+        assert L.rtg_render(h, 0, spp, seed, None, 0) == 0, L.rtg_last_error()
+        film = np.zeros((kw["height"], kw["width"], 3), np.float32)
+        n = C.c_uint32()
+        assert L.rtg_film_read(h, N.ptr(film, C.c_float), C.byref(n)) == 0
+    finally:
+        L.rtg_destroy(h)
+    assert n.value == spp
+    assert_bitexact(film, ref, "reference-side binding (%s)" % case)

@@ -177,3 +177,58 @@ def test_synthetic_1m_matches_reference_loader(tmp_path):
     lights, camera)."""
     write_synthetic_scene(str(tmp_path), n_tris=1_000_000, seed=20251015, width=1024, height=1024)
     _check_digests("synth1m", loadScene(str(tmp_path)))
+
+
+def _desc_arrays(d):
+    """numpy copies of an rtg_scene_desc's arrays (ctypes struct)."""
+    import ctypes as C
+
+    def arr(p, n, dt):
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float if dt == np.float32 else C.c_int32)),
+                                     shape=(n,)).view(dt).copy() if n else np.zeros(0, dt)
+    out = {"positions": arr(d.positions, d.n_tris * 9, np.float32), "normals": arr(d.normals, d.n_tris * 9, np.float32),
+           "uvs": arr(d.uvs, d.n_tris * 6, np.float32), "material": arr(d.material, d.n_tris, np.int32),
+           "node_bounds": arr(d.node_bounds, d.n_nodes * 6, np.float32),
+           "node_links": arr(d.node_links, d.n_nodes * 4, np.int32).reshape(-1, 4),
+           "lights": arr(d.lights, d.n_lights, np.int32),
+           "camera": np.concatenate([np.array(d.camera.inv_proj[:], np.float32), np.array(d.camera.camera[:], np.float32),
+                                     np.array(d.camera.origin[:], np.float32), np.float32([d.camera.width, d.camera.height])]),
+           "projection": np.concatenate([np.array(d.projection.proj[:], np.float32),
+                                         np.array(d.projection.camera_to_view[:], np.float32),
+                                         np.array(d.projection.view_direction[:], np.float32), np.float32([d.projection.a_film])]),
+           "materials": [(m.kind, m.two_sided, m.int_ior, m.ext_ior, tuple(m.emission)) for m in d.materials[:d.n_materials]],
+           "env_texture": d.env_texture}
+    tex = []
+    for i in range(d.n_textures):
+        t = d.textures[i]
+        tex.append(arr(t.texels, t.width * t.height * 3, np.float32).reshape(t.height, t.width, 3))
+    out["textures"] = tex
+    out["mat_tex"] = [m.texture for m in d.materials[:d.n_materials]]
+    return out
+
+
+@pytest.mark.parametrize("case", ["cornell-mat", "cornell-box"])
+def test_reference_side_binding_flattens_like_the_host(case):
+    """integration/rtg_rtbase.h (compiled against the reference headers into
+    oracle/_ref) flattens the reference loader's own Scene into the rtg_scene_desc that librth builds
+    from the same scene.json: the same bits in every array (BVH links compared on the child / leaf
+    fields the ABI reads)."""
+    from oracle import pyref
+    from raytracingrenderer_amd import _native as N
+    if not pyref.available():
+        pytest.skip("oracle/_ref needs /root/reference (build container)")
+    import ctypes as C
+    path = os.path.join(SCENES, case)
+    r = pyref.RefScene(path, 64, 48, False)
+    ref = _desc_arrays(C.cast(r.rtg_desc(), C.POINTER(N.rtg_scene_desc)).contents)
+    s = loadScene(path, width=64, height=48)
+    host = _desc_arrays(s.desc)
+    for k in ("positions", "normals", "uvs", "material", "node_bounds", "lights", "camera", "projection"):
+        assert np.array_equal(ref[k].view(np.uint32), host[k].view(np.uint32)), k
+    assert np.array_equal(ref["node_links"][:, :2], host["node_links"][:, :2])
+    leaf = ref["node_links"][:, 0] < 0
+    assert np.array_equal(ref["node_links"][leaf, 2:], host["node_links"][leaf, 2:])
+    assert ref["materials"] == host["materials"]
+    assert (ref["env_texture"] >= 0) == (host["env_texture"] >= 0)
+    for a, b in zip(ref["mat_tex"], host["mat_tex"]):
+        assert np.array_equal(ref["textures"][a].view(np.uint32), host["textures"][b].view(np.uint32))
