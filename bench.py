@@ -248,6 +248,7 @@ def main():
     for _ in range(a.steps):
         step()
         st = rt.stats()
+        timed_ranks = getattr(rt, "last_ranks", None)
         ext_rays += st["extension_rays"]
         shadow_rays += st["shadow_rays"]
         paths += st["paths"]
@@ -292,7 +293,7 @@ def main():
     local_kernel_ms = (extend_ms, shadow_ms, shade_ms)
     group_info = None
     if group_devs is not None:
-        r0 = rt.last_ranks[0] if rt.last_ranks else {}
+        r0 = timed_ranks[0] if timed_ranks else {}
         local_kernel_ms = (r0.get("extend_ms", 0.0) * a.steps, 0.0, r0.get("shade_ms", 0.0) * a.steps)
         prep_ms, up_ms = rt.g.setup_ms()
         timed_reduce = rt.reduce_ms[a.warmup:a.warmup + a.steps]
@@ -301,7 +302,7 @@ def main():
                                    "parallel_uploads": round(up_ms, 1)},
                       "reduce_ms_per_step": round(float(np.mean(timed_reduce)), 3) if timed_reduce else None,
                       "rank_kernel_ms_last_step": [{"trace": round(r["extend_ms"], 2), "shade": round(r["shade_ms"], 2),
-                                                    "render": round(r["render_ms"], 2)} for r in rt.last_ranks]}
+                                                    "render": round(r["render_ms"], 2)} for r in timed_ranks]}
     totals = np.array([ext_rays, shadow_rays, paths, extend_ms, extend_launches,
                        cs["node_visits"], cs["tri_tests"], cs["extension_rays"],
                        cw["node_visits"], cw["tri_tests"],
