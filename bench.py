@@ -30,8 +30,18 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, same guide (§L2)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")  # rocprofv3 PMC passes of the C3 bench
+KSTATS = os.path.join(ROOT, "profiles", "r03_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
+ROOF_REPLAY = os.path.join(ROOT, "profiles", "r03_roof_replay.jsonl")  # tools/roof_replay.py (C3)
+# k_shade's algorithmic bytes (per path it shades; PATH integrator): reads queue id 4, ray_o 16,
+# ray_d 16, hit 16, throughput 16, meta 4, PCG state 8, pixel 4 and the hit triangle's shading record
+# 64; writes contrib 16 and meta 4; a continuing path also writes ray_o, ray_d, throughput 16 each,
+# PCG 8 and its queue id 4; an NEE sample writes sh_o, sh_d 16 each and its queue id 4. Scene records
+# shared by many paths (materials, lights, texels) are not counted.
+SHADE_B_PATH = 4 + 16 + 16 + 16 + 16 + 4 + 8 + 4 + 64 + 16 + 4
+SHADE_B_CONT = 16 + 16 + 16 + 8 + 4
+SHADE_B_NEE = 16 + 16 + 4
 ROOF_TABLE_MIB = 69  # the hot scene of C3: 21 MB wide nodes + 48 MB triangle records
 HOT_BYTES_PER_TRI = 69.0  # wide nodes (~21 B per triangle on C3) + the 48-B triangle record
 # per-ray queue id + ray origin + direction reads and the hit / visibility write (16-B requests)
@@ -361,16 +371,36 @@ def main():
     achieved_rec = req_totals[1] / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
     ceiling = request_ceiling(scene.desc.n_tris)
     avg_launch_s = extend_ms / max(extend_launches, 1) / 1e3
-    # measured HBM traffic per launch (PMC, profiles/): only for the profiled workload (C3, 64 spp,
-    # one rank); other configs, shards and N > 1 have other launch sizes and report null
-    traffic = None
+    # profiles/ evidence for the profiled workload (C3, 64 spp, one GPU): PMC traffic, kernel-trace
+    # durations, and the locality-matched replay ceiling; other configs / shards / N > 1 report null
+    traffic = pmc = None
     profiled = (a.config == "C3" and world == 1 and group_devs is None and a.shard_of <= 1 and a.spp == 64 and a.tris == 1_000_000
                 and (a.width, a.height) == (1024, 1024) and a.max_depth == 4)
     if profiled and os.path.exists(PMC_SUMMARY):
         try:
-            traffic = json.load(open(PMC_SUMMARY)).get("extend_hbm_bytes_per_launch")
+            pmc = json.load(open(PMC_SUMMARY))
+            traffic = pmc.get("extend_hbm_bytes_per_launch")
         except Exception:
-            traffic = None
+            pmc = None
+    replay = None
+    if profiled and os.path.exists(ROOF_REPLAY):
+        try:
+            replay = [json.loads(l) for l in open(ROOF_REPLAY) if '"total"' in l][-1]
+        except Exception:
+            replay = None
+    # k_shade: algorithmic payload bytes per step (SHADE_B_*) / its kernel time (the timed region's
+    # generate + shade + accumulate HIP events), and the PMC DRAM-level bytes of its launches
+    shaded = ext_rays  # every closest-hit ray's result is shaded once
+    cont = max(ext_rays - paths, 0)  # continuing paths = extension rays after the camera rays
+    shade_algo_bytes = shaded * SHADE_B_PATH + cont * SHADE_B_CONT + shadow_rays * SHADE_B_NEE
+    shade_algo_gbs = shade_algo_bytes / (shade_ms / 1e3) / 1e9 if shade_ms > 0 else None
+    shade_pmc = None
+    if pmc:
+        ks = [v for k, v in pmc.get("kernels", {}).items() if k.startswith("void k_shade<false>")]
+        if ks and ks[0].get("avg_ns_trace"):
+            kb = ks[0]["read_bytes_corrected"] + ks[0]["write_bytes"]
+            shade_pmc = {"bytes_per_launch": kb, "avg_launch_ms": round(ks[0]["avg_ns_trace"] / 1e6, 4),
+                         "achieved_gbs": round(kb / (ks[0]["avg_ns_trace"] / 1e9) / 1e9, 1)}
 
     cpu = None
     if rank == 0 and world == 1 and group_devs is None and not a.no_cpu_baseline:
@@ -407,17 +437,34 @@ def main():
                                                            else "host-memory (repeated devices)"))},
             "roofline": {"bound": "dependent-random-record-fetches", "kernel": "k_trace (extension + shadow rays)",
                          "achieved": None if achieved_rec is None else round(achieved_rec, 1),
-                         "peak": None if ceiling is None else round(ceiling["g_lane_steps_per_s"], 1),
+                         "peak": (round(replay["ceiling_g_fetches_per_s"], 1) if replay else
+                                  None if ceiling is None else round(ceiling["g_lane_steps_per_s"], 1)),
                          "unit": "G dependent random per-lane record fetches/s (node steps + triangle heads + leaf boxes)",
-                         "frac": (round(achieved_rec / ceiling["g_lane_steps_per_s"], 4)
-                                  if achieved_rec and ceiling else None),
+                         "frac": (round(achieved_rec / replay["ceiling_g_fetches_per_s"], 4) if replay and achieved_rec else
+                                  round(achieved_rec / ceiling["g_lane_steps_per_s"], 4) if achieved_rec and ceiling else None),
+                         "peak_is": ("locality-matched in-repo ceiling (not a hardware peak): every launch's own fetch "
+                                     "stream of this workload captured and replayed on the scene's arrays with nothing "
+                                     "else in the loop (tools/roof_replay.py, %s)" % os.path.relpath(ROOF_REPLAY, ROOT)
+                                     if replay else
+                                     "in-repo microbenchmark ceiling (not a hardware peak): uniform random dependent "
+                                     "64-B records (tools/micro/roof.hip, %s)" % os.path.relpath(ROOF_SWEEP, ROOT)),
                          "traffic": traffic,
-                         "ceiling": (None if ceiling is None else
-                                     "tools/micro/roof.hip, %s: dependent random 64-B per-lane records (4 x "
-                                     "dwordx4), %d MiB table, %d VALU/step, k_trace's occupancy (flat from 2 to 16 "
-                                     "waves/SIMD: profiles/r02_roof_occ.jsonl)"
-                                     % (os.path.relpath(ROOF_SWEEP, ROOT), ceiling["table_mib"],
-                                        ceiling["valu_per_step"])),
+                         "traffic_source": (None if traffic is None else
+                                            "%s: rocprofv3 PMC (FETCH_SIZE x1 for the gathers + WRITE_SIZE, DRAM share) "
+                                            "of this workload in separate passes; from profiles/, not measured in this run"
+                                            % os.path.relpath(PMC_SUMMARY, ROOT)),
+                         "frac_uniform_random_ceiling": (round(achieved_rec / ceiling["g_lane_steps_per_s"], 4)
+                                                         if achieved_rec and ceiling else None),
+                         "uniform_random_ceiling": (None if ceiling is None else
+                                                    {"peak": round(ceiling["g_lane_steps_per_s"], 1),
+                                                     "source": "tools/micro/roof.hip, %s: dependent random 64-B per-lane "
+                                                               "records, %d MiB table, %d VALU/step"
+                                                               % (os.path.relpath(ROOF_SWEEP, ROOT), ceiling["table_mib"],
+                                                                  ceiling["valu_per_step"])}),
+                         "replay": (None if not replay else
+                                    {"k_trace_ms": round(replay["k_trace_ms"], 2), "replay_ms": round(replay["replay_ms"], 2),
+                                     "replayed_fetches": replay["replayed_fetches"],
+                                     "frac_at_measurement": round(replay["frac"], 4)}),
                          "fetches_per_ray": round(rec_step / max(all_rays, 1), 2),
                          "requests": {"achieved": None if achieved_req is None else round(achieved_req, 1),
                                       "peak": None if ceiling is None else round(ceiling["g_req_per_s"], 1),
@@ -428,24 +475,25 @@ def main():
                          "tri_tail_loads_per_ray": round(cw["tri_tail_loads"] / max(all_rays, 1), 2),
                          "leafbox_tests_per_ray": round(cw["leafbox_tests"] / max(all_rays, 1), 2),
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                         "hbm": {"bytes_per_launch": traffic,
-                                 "achieved_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic and extend_ms > 0 else None,
-                                 "peak_gbs": HBM_PEAK_GBS,
-                                 "frac": (round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4)
-                                          if traffic and extend_ms > 0 else None),
-                                 "source": "rocprofv3 FETCH_SIZE (x1: calibrated for 64-B gathers, "
-                                           "profiles/r02_fetch_calibration.json) + WRITE_SIZE, per launch"},
-                         "algorithmic": {"definition": "SURVEY.md 8d: 32 B x box tests + 36 B x triangle tests + "
-                                                       "48 B per ray, reference BVH2 walk counts",
-                                         "achieved_gbs": None if algo_gbs is None else round(algo_gbs, 1),
-                                         "served_by": "L1 / L2 / Infinity Cache (scene ~70 MB hot)",
-                                         "l2_peak_gbs": L2_PEAK_GBS,
-                                         "l2_frac": None if algo_gbs is None else round(algo_gbs / L2_PEAK_GBS, 4),
-                                         "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
-                                         "tri_tests_per_ray": round(tris_per_ray, 2),
-                                         "bytes_per_shadow_ray": round(b_sray, 1),
-                                         "shadow_box_tests_per_ray": round(s_boxes_per_ray, 2),
-                                         "shadow_tri_tests_per_ray": round(s_tris_per_ray, 2)},
+                         "hw_peaks": {
+                             "hbm": {"bytes_per_launch": traffic,
+                                     "achieved_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic and extend_ms > 0 else None,
+                                     "peak_gbs": HBM_PEAK_GBS,
+                                     "frac": (round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4)
+                                              if traffic and extend_ms > 0 else None),
+                                     "source": "PMC (traffic_source)"},
+                             "l2_algorithmic": {"definition": "SURVEY.md 8d: 32 B x box tests + 36 B x triangle tests + "
+                                                              "48 B per ray, reference BVH2 walk counts",
+                                                "achieved_gbs": None if algo_gbs is None else round(algo_gbs, 1),
+                                                "served_by": "L1 / L2 / Infinity Cache (scene ~70 MB hot)",
+                                                "peak_gbs": L2_PEAK_GBS,
+                                                "frac": None if algo_gbs is None else round(algo_gbs / L2_PEAK_GBS, 4),
+                                                "frac_of_hbm_peak": None if algo_gbs is None else round(algo_gbs / HBM_PEAK_GBS, 4),
+                                                "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
+                                                "tri_tests_per_ray": round(tris_per_ray, 2),
+                                                "bytes_per_shadow_ray": round(b_sray, 1),
+                                                "shadow_box_tests_per_ray": round(s_boxes_per_ray, 2),
+                                                "shadow_tri_tests_per_ray": round(s_tris_per_ray, 2)}},
                          "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from an own 3-axis SAH tree over the reference leaves)",
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
@@ -457,6 +505,18 @@ def main():
                          "lane_util_node_leaf": [round(cw["node_lane_steps"] / max(cw["lane_slots"], 1), 3),
                                                  round(cw["leaf_lane_steps"] / max(cw["leaf_phase_slots"], 1), 3),
                                                  round(cw["leaf_phase_slots"] / max(cw["lane_slots"], 1), 3)]},
+            "roofline_shade": {"bound": "hbm", "kernel": "k_shade (+ k_generate, k_accumulate in the time)",
+                               "achieved": None if shade_algo_gbs is None else round(shade_algo_gbs, 1),
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": None if shade_algo_gbs is None else round(shade_algo_gbs / HBM_PEAK_GBS, 4),
+                               "algorithmic_bytes_per_step": round(shade_algo_bytes / max(a.steps, 1)),
+                               "definition": "per shaded path %d B (payload reads + hit record + contrib/meta writes), "
+                                             "+%d B per continuing path, +%d B per NEE sample; scene records shared by "
+                                             "paths not counted" % (SHADE_B_PATH, SHADE_B_CONT, SHADE_B_NEE),
+                               "pmc": shade_pmc,
+                               "pmc_source": (None if shade_pmc is None else "%s (k_shade<false>, DRAM-level bytes "
+                                              "FETCH_SIZE x2 + WRITE_SIZE per launch, rocprof kernel-trace duration); "
+                                              "from profiles/, not measured in this run" % os.path.relpath(PMC_SUMMARY, ROOT))},
             "kernel_ms_per_step_rank0": {"trace": round(local_kernel_ms[0] / a.steps, 2),
                                          "generate_shade_accumulate": round(local_kernel_ms[2] / a.steps, 2)},
             "cpu_baseline": cpu,

@@ -237,6 +237,16 @@ int  rtg_film_copy_device(rtg_handle* h, void* dst_device /* width*height*3 floa
 int  rtg_film_load(rtg_handle* h, const float* rgb_sum, uint32_t spp);  /* resume */
 int  rtg_clear(rtg_handle* h);
 int  rtg_get_stats(rtg_handle* h, rtg_stats* out);
+/* Per traversal launch (k_trace) device time of the last render with RTG_OPT_TIMING, in launch
+ * order (chunk by chunk, bounce by bounce): n receives the count, at most max are written. */
+int  rtg_launch_times(rtg_handle* h, double* trace_ms, uint32_t max, uint32_t* n);
+/* Diagnostics of the locality-matched roofline (builds with RTG_DEBUG=1 only; RTG_ERR_ARG
+ * otherwise). rtg_debug_capture(h, b): the next render records every record fetch of trace launch
+ * b of its first chunk, per ray in order (-1: off). rtg_debug_replay(h, out[4]) replays that
+ * stream (same addresses, order, grouping and occupancy; nothing but the fetches and 64 VALU per
+ * step) on the device: out = {best of 3 replay ms, fetches, extension rays, shadow rays}. */
+int  rtg_debug_capture(rtg_handle* h, int launch);
+int  rtg_debug_replay(rtg_handle* h, double* out);
 
 /* Low-level ray queries on the uploaded scene (test / oracle comparison surface).
  * rays: n*8 floats (o.xyz, tmax, dir.xyz, pad). For closest-hit, tmax is ignored and the result

@@ -28,7 +28,9 @@ using namespace rtgd;
 #define RTG_FETCH_TAIL 8    // fetch RTG_TAIL_BATCH rays per atomic once about this many rounds of
 #define RTG_TAIL_BATCH 64   // big batches are left in the slice (shorter drain tails)
 #define RTG_SHADE_WAVES 5   // min waves per SIMD for k_shade (96 VGPRs, no spills)
-// RTG_DEBUG=1 (a diagnostic build only) compiles k_trace's per-wave clocks (RTG_OPT_WAVETIME).
+// RTG_DEBUG=1 (a diagnostic build only) compiles k_trace's per-wave clocks (RTG_OPT_WAVETIME) and
+// the fetch capture + replay of the locality-matched roofline (RTG_OPT_CAPTURE, rtg_debug_replay).
+#define RTG_CAP_LEN 64
 #ifndef RTG_DEBUG
 #define RTG_DEBUG 0
 #endif
@@ -68,6 +70,11 @@ struct TraceIO {
     int cull;
     int wide;                  // traverse the 4-wide tree when the ray allows it
     unsigned long long* wtime; // RTG_DEBUG builds: per wave start / drained / exit clock
+    uint4* cap;                // RTG_DEBUG builds (RTG_OPT_CAPTURE): every ray's record fetches,
+                               // [k / 4][ray] uint4 (type << 30 | index; type 0 wide node, 1 triangle
+                               // head, 2 leaf box, 3 BVH2 node), at most RTG_CAP_LEN per ray
+    unsigned* cap_len;         // [ray] fetches captured (<= RTG_CAP_LEN)
+    unsigned cap_n;            // rays the capture holds (work index space of the launch)
     float4 cam_o;              // closest: the origin of every ray when ray_o is null (camera rays);
                                // a null queue is the identity (path id = ray index)
 };
@@ -147,6 +154,12 @@ struct rtg_handle {
     uint32_t max_paths = 1u << 30;  // 1G paths in flight at most; the chunk is held to half the free HBM
     int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0;
     int wavetime = 0;  // RTG_DEBUG builds: per-wave clocks of the first chunk (RTG_OPT_WAVETIME)
+    int capture_launch = -1;  // RTG_DEBUG builds: trace launch of chunk 0 whose fetches are captured
+    uint4* d_cap = nullptr;           // its chains (TraceIO::cap)
+    unsigned* d_cap_len = nullptr;    // its chain lengths
+    unsigned* d_cap_rays = nullptr;   // [2]: its extension and shadow ray counts
+    unsigned cap_n = 0;               // rays the capture buffers hold
+    std::vector<double> launch_ms;    // per trace launch of the last timed render (RTG_OPT_TIMING)
     uint32_t bvh_depth = 0;
     SceneView sv{};
     DevCamera cam{};

@@ -72,6 +72,22 @@ void k_trace(SceneView s, TraceIO io) {
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0, pend = RTG_EXIT;
     bool occluded = false, wide = false, anyr = false;  // anyr: this lane's ray is a shadow ray
     const unsigned wslot = gtid >> 6;
+    // RTG_DEBUG capture: the ray's record fetches in order (cap_k of them so far)
+    unsigned cap_ri = 0, cap_k = 0;
+    uint4 cap_q = make_uint4(0, 0, 0, 0);
+    auto capture = [&](unsigned type, unsigned idx) {
+        if (!RTG_DEBUG || !io.cap) return;
+        if (cap_k < RTG_CAP_LEN) {
+            const unsigned e = (type << 30) | idx;
+            const unsigned j = cap_k & 3;
+            cap_q.x = j == 0 ? e : cap_q.x;
+            cap_q.y = j == 1 ? e : cap_q.y;
+            cap_q.z = j == 2 ? e : cap_q.z;
+            cap_q.w = j == 3 ? e : cap_q.w;
+            if (j == 3) io.cap[(size_t)(cap_k >> 2) * io.cap_n + cap_ri] = cap_q;
+        }
+        ++cap_k;
+    };
     if (RTG_DEBUG && io.wtime && lane == 0) io.wtime[3 * wslot] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         // ---- retire finished rays
@@ -82,6 +98,11 @@ void k_trace(SceneView s, TraceIO io) {
                     io.contrib[pid] = bid == -2 ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : io.sray_c[pid];
             } else {
                 io.hits[pid] = make_float4(tbest, __int_as_float(bid), bu, bv);
+            }
+            if (RTG_DEBUG && io.cap) {
+                const unsigned k = min(cap_k, (unsigned)RTG_CAP_LEN);
+                if (k & 3) io.cap[(size_t)(k >> 2) * io.cap_n + cap_ri] = cap_q;
+                io.cap_len[cap_ri] = cap_k;  // the true count; the first RTG_CAP_LEN are kept
             }
             have = false;
         }
@@ -126,6 +147,7 @@ void k_trace(SceneView s, TraceIO io) {
                         ri = j < e_len ? e_lo + j : nc + (unsigned)(((unsigned long long)ns * (unsigned)slice) >> 3) + (j - e_len);
                     }
                     have = true;
+                    if (RTG_DEBUG) { cap_ri = ri; cap_k = 0; }
                     anyr = ri >= nc;
                     pid = (int)(anyr ? io.squeue[ri - nc] : (io.queue ? io.queue[ri] : ri));
                     const float4 ro = anyr ? io.sray_o[pid] : (io.ray_o ? io.ray_o[pid] : io.cam_o);
@@ -174,6 +196,7 @@ void k_trace(SceneView s, TraceIO io) {
             for (int k = 0; k < cnt; ++k) {
                 const int tri = start + k;
                 if (COUNT) (anyr ? c_stris : c_tris) += 1;
+                capture(1u, (unsigned)tri);
                 float t, u, v;
                 const bool hit = tri_intersect48p(s.tris48 + tri, o, d, [&](float tt) {
                     return anyr ? (tt < tbest && tt > RTG_EPS) : (tt <= tbest && tt > RTG_EPS);
@@ -186,6 +209,7 @@ void k_trace(SceneView s, TraceIO io) {
                         // triangle: a wide leaf slot may join sibling reference leaves)
                         const float4 b0 = s.leafbox[2 * tri], b1 = s.leafbox[2 * tri + 1];
                         if (COUNT) c_lbox += 1;
+                        capture(2u, (unsigned)tri);
                         cand = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
                     }
                     if (!cand) {
@@ -206,6 +230,7 @@ void k_trace(SceneView s, TraceIO io) {
             int wd[4];
             float key[4];
             {
+                capture(0u, (unsigned)cur);
                 const float4* np = s.nodesq[cur].q;
                 const float4 h0 = np[0], h1 = np[1], h2 = np[2], h3 = np[3];
                 const unsigned ex = __float_as_uint(h0.w);
@@ -304,6 +329,7 @@ void k_trace(SceneView s, TraceIO io) {
             }
         } else if (cur >= 0) {
             if (COUNT) (anyr ? c_snodes : c_nodes) += 2;
+            capture(3u, (unsigned)cur);
             const DevNode nd = s.nodes[cur];
             bool hl = slab_exact(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, o, inv);
             bool hr = slab_exact(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, o, inv);
@@ -396,6 +422,97 @@ void k_trace(SceneView s, TraceIO io) {
         }
     }
 }
+
+#if RTG_DEBUG
+// ------------------------------------------------------------------ locality-matched ceiling
+// Replays the record fetches k_trace made for every ray of one launch (captured in order by
+// RTG_OPT_CAPTURE) on the scene's own arrays: the same record types, addresses, per-ray order and
+// ray-to-lane grouping, with nothing else in the loop but the fetch of the next chain entry (one
+// coalesced uint4 per four steps) and 64 dependent VALU per step, at k_trace's occupancy and with
+// its work distribution (8 slice counters by blockIdx % 8, 64-ray pool batches, per-lane refill).
+// Each fetch's address depends on the previous record's data (xor with `zero` = 0 at run time), so
+// every ray is one dependent chain, as in the walk. Its time is the memory system's time for this
+// exact access stream: the ceiling k_trace's time is compared against.
+__global__ __launch_bounds__(RTG_TB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
+void k_replay(SceneView s, const uint4* cap, const unsigned* cap_len, unsigned n, unsigned cap_n, unsigned zero,
+              unsigned* fetch8, unsigned long long* total, float* out) {
+    const int lane = lane_id();
+    const int slice0 = (int)(blockIdx.x & 7u);
+    int slice = slice0, tried = 0;
+    auto slo = [&](int k) { return (unsigned)(((unsigned long long)n * (unsigned)k) >> 3); };
+    unsigned s_lo = slo(slice), s_len = slo(slice + 1) - s_lo;
+    unsigned pool_base = 0, pool_left = 0;
+    bool drained = false, have = false;
+    unsigned ri = 0, k = 0, len = 0, dep = 0;
+    uint4 q = make_uint4(0, 0, 0, 0);
+    float acc = 0.0f;
+    unsigned long long fetches = 0;
+    for (;;) {
+        const unsigned long long im = __ballot(!have);
+        if (im != 0 && !drained) {
+            while (pool_left == 0) {
+                unsigned b = 0;
+                if (lane == 0) b = atomicAdd(fetch8 + 32 * slice, 64u);
+                b = __builtin_amdgcn_readfirstlane(b);
+                if (b < s_len) {
+                    pool_base = s_lo + b;
+                    pool_left = min(64u, s_len - b);
+                } else if (++tried == 8) {
+                    drained = true;
+                    break;
+                } else {
+                    slice = (slice + 1) & 7;
+                    s_lo = slo(slice);
+                    s_len = slo(slice + 1) - s_lo;
+                }
+            }
+            if (pool_left > 0) {
+                const unsigned pos = prefix_lt(im);
+                const unsigned take = min((unsigned)__popcll(im), pool_left);
+                if (!have && pos < take) {
+                    ri = pool_base + pos;
+                    len = min(cap_len[ri], (unsigned)RTG_CAP_LEN);
+                    k = 0;
+                    have = len > 0;
+                }
+                pool_base += take;
+                pool_left -= take;
+            }
+        }
+        if (drained && __ballot(have) == 0) break;
+        if (!have) continue;
+        if ((k & 3) == 0) q = cap[(size_t)(k >> 2) * cap_n + ri];
+        const unsigned j = k & 3;
+        const unsigned e = (j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w) ^ (dep & zero);
+        const unsigned type = e >> 30, idx = e & 0x3fffffffu;
+        float sum;
+        if (type == 0) {
+            const float4* r = s.nodesq[idx].q;
+            const float4 a = r[0], b = r[1], c = r[2], d = r[3];
+            sum = (((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w))) + (((c.x + c.y) + (c.z + c.w)) + ((d.x + d.y) + (d.z + d.w)));
+        } else if (type == 1) {
+            const float4 a = s.tris48[idx].a, b = s.tris48[idx].b;  // the head: n and v0 decide t
+            sum = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+        } else if (type == 2) {
+            const float4 a = s.leafbox[2 * idx], b = s.leafbox[2 * idx + 1];
+            sum = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+        } else {
+            const DevNode nd = s.nodes[idx];
+            sum = (((nd.a.x + nd.a.y) + (nd.a.z + nd.a.w)) + ((nd.b.x + nd.b.y) + (nd.b.z + nd.b.w))) +
+                  (((nd.c.x + nd.c.y) + (nd.c.z + nd.c.w)) + __int_as_float(nd.d.x ^ nd.d.y));
+        }
+#pragma unroll
+        for (int v = 0; v < 64; ++v) sum = __builtin_fmaf(sum, 1.0000001f, (float)v);
+        acc += sum;
+        dep = __float_as_uint(sum);
+        ++fetches;
+        if (++k == len) have = false;
+    }
+    for (int off = 32; off > 0; off >>= 1) fetches += __shfl_down(fetches, off);
+    if (lane == 0) atomicAdd(total, fetches);
+    if (acc == 1.2345f) out[0] = acc;  // keep the loads
+}
+#endif
 
 // ------------------------------------------------------------------ generate
 __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
@@ -1446,6 +1563,7 @@ void rtg_destroy(rtg_handle* h) {
     (void)hipFree(h->d_pix); (void)hipFree(h->d_ovf); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
     for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : h->kev) (void)hipEventDestroy(e);
+    (void)hipFree(h->d_cap); (void)hipFree(h->d_cap_len); (void)hipFree(h->d_cap_rays);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1634,6 +1752,26 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             io.fetch = &pb.ctr[b].f_ext;
             io.fetch8 = pb.ctr[b].f8;
             io.wtime = (d_wt && c == 0) ? d_wt + (size_t)b * wt_waves * 3 : nullptr;
+            io.cap = nullptr;
+            io.cap_len = nullptr;
+            if (RTG_DEBUG && c == 0 && b == h->capture_launch) {
+                const size_t cn = (size_t)a.P * (b == 0 ? 1 : 2);
+                (void)hipFree(h->d_cap);
+                (void)hipFree(h->d_cap_len);
+                h->d_cap = nullptr;
+                h->d_cap_len = nullptr;
+                HIPOK(hipMalloc((void**)&h->d_cap, cn * (RTG_CAP_LEN / 4) * sizeof(uint4)));
+                HIPOK(hipMalloc((void**)&h->d_cap_len, cn * sizeof(unsigned)));
+                if (!h->d_cap_rays) HIPOK(hipMalloc((void**)&h->d_cap_rays, 2 * sizeof(unsigned)));
+                HIPOK(hipMemsetAsync(h->d_cap_len, 0, cn * sizeof(unsigned), st));
+                HIPOK(hipMemsetAsync(h->d_cap_rays, 0, 2 * sizeof(unsigned), st));
+                if (io.count) HIPOK(hipMemcpyAsync(h->d_cap_rays, io.count, 4, hipMemcpyDeviceToDevice, st));
+                if (io.scount) HIPOK(hipMemcpyAsync(h->d_cap_rays + 1, io.scount, 4, hipMemcpyDeviceToDevice, st));
+                h->cap_n = (unsigned)cn;
+                io.cap = h->d_cap;
+                io.cap_len = h->d_cap_len;
+                io.cap_n = (unsigned)cn;
+            }
             timed_begin(h, st, k);
             if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
             else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
@@ -1687,11 +1825,15 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         HIPOK(hipEventSynchronize(h->ev[1]));
         h->stats.extend_ms = h->stats.shadow_ms = h->stats.shade_ms = 0;
         h->stats.extend_launches = 0;
+        h->launch_ms.clear();
         for (size_t j = 0; j < kinds.size(); ++j) {
             float ms = 0;
             (void)hipEventElapsedTime(&ms, h->kev[2 * j], h->kev[2 * j + 1]);
             (kinds[j] == 0 ? h->stats.extend_ms : h->stats.shade_ms) += ms;
-            if (kinds[j] == 0) h->stats.extend_launches++;
+            if (kinds[j] == 0) {
+                h->stats.extend_launches++;
+                h->launch_ms.push_back(ms);
+            }
         }
     }
     return RTG_OK;
@@ -1805,6 +1947,70 @@ int rtg_render_adaptive(rtg_handle* h, uint32_t first, uint64_t seed, uint32_t i
     (void)hipFree(d_tmp);
     h->spp = spp0 + 1;  // render(): film->incrementSPP() once per frame
     return RTG_OK;
+}
+
+int rtg_launch_times(rtg_handle* h, double* trace_ms, uint32_t max, uint32_t* n) {
+    if (!h || !n) return RTG_ERR_ARG;
+    *n = (uint32_t)h->launch_ms.size();
+    for (uint32_t i = 0; trace_ms && i < std::min<uint32_t>(max, *n); ++i) trace_ms[i] = h->launch_ms[i];
+    return RTG_OK;
+}
+
+int rtg_debug_capture(rtg_handle* h, int launch) {
+    if (!h) return RTG_ERR_ARG;
+    if (!RTG_DEBUG) { g_err = "rtg_debug_capture: diagnostic builds only (RTG_DEBUG=1)"; return RTG_ERR_ARG; }
+    h->capture_launch = launch;
+    return RTG_OK;
+}
+
+int rtg_debug_replay(rtg_handle* h, double* out) {
+    if (!h || !out) return RTG_ERR_ARG;
+#if RTG_DEBUG
+    if (!h->d_cap) { g_err = "rtg_debug_replay: nothing captured"; return RTG_ERR_ARG; }
+    HIPOK(hipSetDevice(h->device));
+    HIPOK(hipStreamSynchronize(h->stream));
+    unsigned rays[2] = {0, 0};
+    HIPOK(hipMemcpy(rays, h->d_cap_rays, sizeof(rays), hipMemcpyDeviceToHost));
+    const unsigned n = rays[0] + rays[1];
+    unsigned* d_f8 = nullptr;
+    unsigned long long* d_tot = nullptr;
+    float* d_out = nullptr;
+    HIPOK(hipMalloc((void**)&d_f8, 8 * 32 * sizeof(unsigned)));
+    HIPOK(hipMalloc((void**)&d_tot, sizeof(unsigned long long)));
+    HIPOK(hipMalloc((void**)&d_out, sizeof(float)));
+    hipEvent_t e0, e1;
+    HIPOK(hipEventCreate(&e0));
+    HIPOK(hipEventCreate(&e1));
+    float best = 1e30f;
+    unsigned long long tot = 0;
+    for (int rep = 0; rep < 3; ++rep) {
+        HIPOK(hipMemsetAsync(d_f8, 0, 8 * 32 * sizeof(unsigned), h->stream));
+        HIPOK(hipMemsetAsync(d_tot, 0, sizeof(unsigned long long), h->stream));
+        HIPOK(hipEventRecord(e0, h->stream));
+        hipLaunchKernelGGL(k_replay, dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, (const uint4*)h->d_cap,
+                           (const unsigned*)h->d_cap_len, n, h->cap_n, 0u, d_f8, d_tot, d_out);
+        LAUNCH_OK("k_replay");
+        HIPOK(hipEventRecord(e1, h->stream));
+        HIPOK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIPOK(hipEventElapsedTime(&ms, e0, e1));
+        best = std::min(best, ms);
+        HIPOK(hipMemcpy(&tot, d_tot, sizeof(tot), hipMemcpyDeviceToHost));
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(d_f8);
+    (void)hipFree(d_tot);
+    (void)hipFree(d_out);
+    out[0] = best;
+    out[1] = (double)tot;
+    out[2] = rays[0];
+    out[3] = rays[1];
+    return RTG_OK;
+#else
+    g_err = "rtg_debug_replay: diagnostic builds only (RTG_DEBUG=1)";
+    return RTG_ERR_ARG;
+#endif
 }
 
 int rtg_synchronize(rtg_handle* h) {
