@@ -27,7 +27,9 @@ using namespace rtgd;
 #define RTG_FETCH 256       // rays a wave takes from a work counter per atomic (k_trace pool)
 #define RTG_FETCH_TAIL 8    // fetch RTG_TAIL_BATCH rays per atomic once about this many rounds of
 #define RTG_TAIL_BATCH 64   // big batches are left in the slice (shorter drain tails)
+#ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 5   // min waves per SIMD for k_shade (96 VGPRs, no spills)
+#endif
 // RTG_DEBUG=1 (a diagnostic build only) compiles k_trace's per-wave clocks (RTG_OPT_WAVETIME) and
 // the fetch capture + replay of the locality-matched roofline (RTG_OPT_CAPTURE, rtg_debug_replay).
 #define RTG_CAP_LEN 64
@@ -51,7 +53,8 @@ struct __align__(16) Counters {
 // One traversal launch serves two ray sets: extension (closest-hit) rays take work indices
 // [0, nc) and NEE shadow (any-hit) rays [nc, nc + ns). Each lane carries its ray's kind.
 struct TraceIO {
-    const unsigned* queue;     // closest: path ids to trace
+    const unsigned* queue;     // closest: path ids to trace (null: the ray at position i is path i;
+                               // the path tracer keeps its extension payload in queue order)
     const float4* ray_o;       // closest: [pid] origin.xyz
     const float4* ray_d;       // closest: [pid] direction.xyz
     const unsigned* count;     // closest: number of rays (device; null = none)
@@ -92,14 +95,20 @@ struct ChunkArgs {
 };
 
 struct PathBufs {
-    float4* thr;               // [P] throughput
+    // extension payload, two sets (the path tracer's bounce b reads set b & 1 by queue position and
+    // writes set (b + 1) & 1; the light tracer / instant radiosity use set 0 by path id)
+    float4* thr;               // [P] throughput (.w: computeDirectMIS's BSDF pdf)
     unsigned long long* rng;   // [P] PCG state
-    int* meta;                 // [P] nterms | canHitLight << 8
-    float4* contrib;           // [maxb][P] per-vertex radiance terms
-    float4* ray_o;             // [P] current extension ray origin
-    float4* ray_d;             // [P] current extension ray direction
-    float4* hits;              // [P] its closest hit (t, id, alpha, beta)
-    float4* sh_o;              // [P] NEE shadow ray origin + maxT
+    float4* ray_o;             // [P] extension ray origin (.w: path id, path tracer)
+    float4* ray_d;             // [P] extension ray direction (.w: canHitLight, path tracer)
+    float4* thr2;              // set 1
+    unsigned long long* rng2;
+    float4* ray_o2;
+    float4* ray_d2;
+    int* meta;                 // [P] by path id: nterms | canHitLight << 8
+    float4* contrib;           // [maxb][P] by path id: per-vertex radiance terms
+    float4* hits;              // [P] closest hit (t, id, alpha, beta) of the ray at queue position i
+    float4* sh_o;              // [P] NEE shadow ray origin + maxT (at its shadow-queue position)
     float4* sh_d;              // [P] NEE shadow ray direction
     float4* sh_c;              // [P] NEE value thr * Ld if visible
     unsigned* q[2];            // extension queues of path ids (ping-pong)

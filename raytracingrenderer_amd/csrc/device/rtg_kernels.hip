@@ -548,6 +548,14 @@ __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
 }
 
 // ------------------------------------------------------------------ shade
+// Path state travels with the queues: the extension payload of bounce b (origin with the path id
+// in .w, direction with canHitLight in .w, throughput, PCG state) sits at the ray's position in
+// the extension queue, in buffer set b & 1. k_trace and k_shade read it by position (contiguous, no
+// id -> payload indirection in either kernel's dependent chain); k_shade writes a continuing
+// path's next payload at its position in set (b + 1) & 1. NEE shadow rays stay indexed by path id
+// (the shadow queue lists the ids): their payload is computed before the BSDF sample and held in
+// registers across it until the compaction, it spilled. Per-path results (contrib, meta) stay
+// indexed by path id for k_accumulate.
 // ALT = false: pathTrace only (RayTracer::render's estimator; the other modes compile away).
 // ALT = true: every per-pixel estimator of rtg_set_integrator, selected by a.mode.
 template <bool ALT>
@@ -556,30 +564,41 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
     __shared__ unsigned s_base[2];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-    const unsigned n = p.ctr[b].n_ext;
-    const unsigned* qin = p.q[b & 1];
-    unsigned* qout = p.q[(b + 1) & 1];
+    const bool lean0 = b == 0;  // bounce 0: path id = position, camera origin, thr 1, PCG seed, canHitLight
+    const unsigned n = lean0 ? a.P : p.ctr[b].n_ext;
+    // extension payload of this bounce (set b & 1, by queue position) and of the next (set (b+1) & 1)
+    const float4* in_o = (b & 1) ? p.ray_o2 : p.ray_o;
+    const float4* in_d = (b & 1) ? p.ray_d2 : p.ray_d;
+    const float4* in_t = (b & 1) ? p.thr2 : p.thr;
+    const unsigned long long* in_r = (b & 1) ? p.rng2 : p.rng;
+    float4* out_o = (b & 1) ? p.ray_o : p.ray_o2;
+    float4* out_d = (b & 1) ? p.ray_d : p.ray_d2;
+    float4* out_t = (b & 1) ? p.thr : p.thr2;
+    unsigned long long* out_r = (b & 1) ? p.rng : p.rng2;
     float4* contrib = p.contrib + (size_t)b * a.P;
-    const bool lean0 = a.lean && b == 0;  // bounce 0: identity queue, state as k_generate would write it
     // block-uniform loop: all waves of a block take part in every compaction round (the launch has
     // one 256-path tile per block: a finished block frees its slot for the next tile)
     for (unsigned base = blockIdx.x * RTG_TB; base < n; base += gridDim.x * RTG_TB) {
         const unsigned i = base + threadIdx.x;
         int pid = 0;
         bool want_ext = false, want_sh = false;
+        // the next bounce's payload, written at its queue position once the block's compaction has
+        // assigned it (the NEE shadow ray is written at once, by path id)
+        float4 n_o = make_float4(0.0f, 0.0f, 0.0f, 0.0f), n_d = n_o, n_t = n_o;
+        unsigned long long n_r = 0;
         const bool valid = i < n;
         if (valid) {
-            pid = lean0 ? (int)i : (int)qin[i];
-            const float4 ro = lean0 ? make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f) : p.ray_o[pid];
-            const float4 rd = p.ray_d[pid];
-            const float4 h = p.hits[pid];
+            const float4 ro = lean0 ? make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f) : in_o[i];
+            pid = lean0 ? (int)i : __float_as_int(ro.w);  // the path id travels in ray_o.w
+            const float4 rd = in_d[i];
+            const float4 h = p.hits[i];
             const v3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
-            const float4 thr4 = lean0 ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : p.thr[pid];
+            const float4 thr4 = lean0 ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : in_t[i];
             v3 thr = mk(thr4.x, thr4.y, thr4.z);
-            const int can_hit = lean0 ? 1 : (p.meta[pid] >> 8) & 1;
+            const int can_hit = lean0 ? 1 : (rd.w != 0.0f);  // canHitLight travels in ray_d.w
             const unsigned lp = (unsigned)pid / a.ns, sl = (unsigned)pid % a.ns;
             const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);
-            uint64_t st = lean0 ? pcg_seed(a.seed, inc) : p.rng[pid];
+            uint64_t st = lean0 ? pcg_seed(a.seed, inc) : in_r[i];
             v3 c;
             int nterms = b + 1;
             if (ALT && a.mode == RTG_INTEGRATOR_DIRECT_MIS && b == 1) {
@@ -709,9 +728,10 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                                                    val, pdf_b);
                         st = smp.s;
                         const v3 no = add(x, muls(wib, RTG_EPS));
-                        p.ray_o[pid] = make_float4(no.x, no.y, no.z, 0.0f);
-                        p.ray_d[pid] = make_float4(wib.x, wib.y, wib.z, 0.0f);
-                        p.thr[pid] = make_float4(val.x, val.y, val.z, pdf_b);
+                        n_o = make_float4(no.x, no.y, no.z, __int_as_float(pid));
+                        n_d = make_float4(wib.x, wib.y, wib.z, 0.0f);
+                        n_t = make_float4(val.x, val.y, val.z, pdf_b);
+                        n_r = st;
                         p.contrib[(size_t)2 * a.P + pid] = make_float4(x.x, x.y, x.z, pdf * pmf);
                         p.contrib[(size_t)3 * a.P + pid] = make_float4(wmax(0.0f, dot(wib, sn)), env_flag, 0.0f, 0.0f);
                         want_ext = true;
@@ -795,11 +815,11 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                             if (spec) thr = divs(mul(thr, ind), pdf);
                             else thr = divs(muls(mul(thr, ind), fabsf(dot(wi, sn))), pdf);
                             const v3 no = add(x, muls(wi, RTG_EPS));
-                            p.ray_o[pid] = make_float4(no.x, no.y, no.z, 0.0f);
-                            p.ray_d[pid] = make_float4(wi.x, wi.y, wi.z, 0.0f);
+                            n_o = make_float4(no.x, no.y, no.z, __int_as_float(pid));
+                            n_d = make_float4(wi.x, wi.y, wi.z, spec ? 1.0f : 0.0f);  // canHitLight
                             want_ext = true;
-                            p.thr[pid] = make_float4(thr.x, thr.y, thr.z, 0.0f);
-                            p.rng[pid] = st;
+                            n_t = make_float4(thr.x, thr.y, thr.z, 0.0f);
+                            n_r = st;
                             nterms = (b + 1) | ((spec ? 1 : 0) << 8);
                         }
                     }
@@ -831,7 +851,13 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             oe += s_cnt[0][w];
             os += s_cnt[1][w];
         }
-        if (want_ext) qout[oe + prefix_lt(me)] = (unsigned)pid;
+        if (want_ext) {
+            const unsigned j = oe + prefix_lt(me);
+            out_o[j] = n_o;
+            out_d[j] = n_d;
+            out_t[j] = n_t;
+            out_r[j] = n_r;
+        }
         if (want_sh) p.shq[os + prefix_lt(ms)] = (unsigned)pid;
         __syncthreads();
     }
@@ -963,6 +989,7 @@ static void free_chunk(rtg_handle* h) {
     (void)hipFree(p.thr); (void)hipFree(p.rng); (void)hipFree(p.meta); (void)hipFree(p.contrib);
     (void)hipFree(p.q[0]); (void)hipFree(p.q[1]); (void)hipFree(p.hits); (void)hipFree(p.shq); (void)hipFree(p.ctr);
     (void)hipFree(p.ray_o); (void)hipFree(p.ray_d);
+    (void)hipFree(p.thr2); (void)hipFree(p.rng2); (void)hipFree(p.ray_o2); (void)hipFree(p.ray_d2);
     (void)hipFree(p.sh_o); (void)hipFree(p.sh_d); (void)hipFree(p.sh_c);
     p = PathBufs{};
     h->cap_P = 0;
@@ -983,6 +1010,10 @@ int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
     HIPOK(hipMalloc((void**)&p.hits, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.ray_o, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.ray_d, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.thr2, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.rng2, P * sizeof(unsigned long long)));
+    HIPOK(hipMalloc((void**)&p.ray_o2, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.ray_d2, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.sh_o, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.sh_d, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.sh_c, P * sizeof(float4)));
@@ -1664,7 +1695,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         // path state of a chunk takes at most half the free HBM (buffers held now count as free)
         size_t freeb = 0, totalb = 0;
         if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
-            auto path_bytes = [](int pl) { return (size_t)152 + (size_t)16 * (size_t)pl; };
+            auto path_bytes = [](int pl) { return (size_t)208 + (size_t)16 * (size_t)pl; };
             const size_t held = h->cap_P * path_bytes(h->cap_maxb);
             const size_t budget = (freeb + held) / 2;
             const size_t max_ns = budget / path_bytes(planes) / std::max<size_t>(1, h->npix);
@@ -1736,10 +1767,12 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                 LAUNCH_OK("k_shade");
                 timed_end(h, st, k); kinds.push_back(2); ++k;
             }
-            io.queue = b == 0 ? nullptr : pb.q[b & 1];  // bounce 0: identity queue, camera origin
-            io.ray_o = b == 0 ? nullptr : pb.ray_o;
+            // extension payload by queue position (set b & 1; null queue: path id = position);
+            // bounce 0: the camera origin, directions from k_generate in set 0
+            io.queue = nullptr;
+            io.ray_o = b == 0 ? nullptr : ((b & 1) ? pb.ray_o2 : pb.ray_o);
             io.cam_o = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f);
-            io.ray_d = pb.ray_d;
+            io.ray_d = (b & 1) ? pb.ray_d2 : pb.ray_d;
             io.count = b < maxb ? &pb.ctr[b].n_ext : nullptr;
             io.hits = pb.hits;
             io.squeue = pb.shq;
