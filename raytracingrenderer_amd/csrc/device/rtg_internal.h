@@ -63,6 +63,8 @@ struct TraceIO {
     const float4* sray_o;      // any-hit: [pid] origin.xyz, w = maxT
     const float4* sray_d;      // any-hit: [pid] direction.xyz
     const float4* sray_c;      // any-hit: [pid] NEE value copied to contrib[pid] when visible
+    int spos;                  // any-hit rays (sray_o, sray_d) at their shadow-queue position (path
+                               // tracer); 0: by path id (light tracer, queries)
     const unsigned* scount;    // any-hit: number of rays (device; null = none)
     float4* contrib;           // any-hit: this bounce's contribution plane [pid]
     int* visible;              // any-hit query output [pid] (instead of contrib)
@@ -108,9 +110,9 @@ struct PathBufs {
     int* meta;                 // [P] by path id: nterms | canHitLight << 8
     float4* contrib;           // [maxb][P] by path id: per-vertex radiance terms
     float4* hits;              // [P] closest hit (t, id, alpha, beta) of the ray at queue position i
-    float4* sh_o;              // [P] NEE shadow ray origin + maxT (at its shadow-queue position)
-    float4* sh_d;              // [P] NEE shadow ray direction
-    float4* sh_c;              // [P] NEE value thr * Ld if visible
+    float4* sh_o;              // [P] NEE shadow ray origin + maxT (path tracer: at its shadow-queue position)
+    float4* sh_d;              // [P] NEE shadow ray direction (same)
+    float4* sh_c;              // [P] by path id: NEE value thr * Ld if visible
     unsigned* q[2];            // extension queues of path ids (ping-pong)
     unsigned* shq;             // shadow queue of path ids
     Counters* ctr;             // [maxb + 1]

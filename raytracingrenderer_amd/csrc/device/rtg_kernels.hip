@@ -150,8 +150,11 @@ void k_trace(SceneView s, TraceIO io) {
                     if (RTG_DEBUG) { cap_ri = ri; cap_k = 0; }
                     anyr = ri >= nc;
                     pid = (int)(anyr ? io.squeue[ri - nc] : (io.queue ? io.queue[ri] : ri));
-                    const float4 ro = anyr ? io.sray_o[pid] : (io.ray_o ? io.ray_o[pid] : io.cam_o);
-                    const float4 rd = anyr ? io.sray_d[pid] : io.ray_d[pid];
+                    // io.spos: the shadow ray sits at its shadow-queue position (no dependence on the
+                    // id load; the id is needed when the ray retires)
+                    const unsigned sk = io.spos ? ri - nc : (unsigned)pid;
+                    const float4 ro = anyr ? io.sray_o[sk] : (io.ray_o ? io.ray_o[pid] : io.cam_o);
+                    const float4 rd = anyr ? io.sray_d[sk] : io.ray_d[pid];
                     // sh_d.w != 0: the shadow value is in sray_c and is copied on visibility;
                     // 0: k_shade already stored it in contrib, which is cleared on occlusion
                     // (kept in bid, which a shadow ray does not use: -2 = value already in contrib)
@@ -552,16 +555,17 @@ __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
 // in .w, direction with canHitLight in .w, throughput, PCG state) sits at the ray's position in
 // the extension queue, in buffer set b & 1. k_trace and k_shade read it by position (contiguous, no
 // id -> payload indirection in either kernel's dependent chain); k_shade writes a continuing
-// path's next payload at its position in set (b + 1) & 1. NEE shadow rays stay indexed by path id
-// (the shadow queue lists the ids): their payload is computed before the BSDF sample and held in
-// registers across it until the compaction, it spilled. Per-path results (contrib, meta) stay
-// indexed by path id for k_accumulate.
+// path's next payload at its position in set (b + 1) & 1 and an NEE ray (staged in LDS: held in
+// registers across the BSDF sample it spilled) at its shadow-queue position, the path id beside
+// it. Per-path results (contrib, meta, and sh_c, the rare copy-on-visible NEE value) stay indexed by
+// path id for k_accumulate.
 // ALT = false: pathTrace only (RayTracer::render's estimator; the other modes compile away).
 // ALT = true: every per-pixel estimator of rtg_set_integrator, selected by a.mode.
 template <bool ALT>
 __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
     __shared__ unsigned s_cnt[2][RTG_TB / 64];
     __shared__ unsigned s_base[2];
+    __shared__ float4 s_sho[RTG_TB], s_shd[RTG_TB];  // NEE ray staged until its queue position is known
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     const bool lean0 = b == 0;  // bounce 0: path id = position, camera origin, thr 1, PCG seed, canHitLight
@@ -597,7 +601,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             v3 thr = mk(thr4.x, thr4.y, thr4.z);
             const int can_hit = lean0 ? 1 : (rd.w != 0.0f);  // canHitLight travels in ray_d.w
             const unsigned lp = (unsigned)pid / a.ns, sl = (unsigned)pid % a.ns;
-            const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);
+            const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);  // (carrying it in the payload: slower)
             uint64_t st = lean0 ? pcg_seed(a.seed, inc) : in_r[i];
             v3 c;
             int nterms = b + 1;
@@ -695,8 +699,8 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                                 const float maxt = sqrtf(length_sq(sd)) - (2.0f * RTG_EPS);
                                 sd = normalize(sd);
                                 const v3 so = add(x, muls(sd, RTG_EPS));
-                                p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
-                                p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 1.0f);  // copy sh_c if visible
+                                s_sho[threadIdx.x] = make_float4(so.x, so.y, so.z, maxt);
+                                s_shd[threadIdx.x] = make_float4(sd.x, sd.y, sd.z, 1.0f);  // copy sh_c if visible
                                 p.sh_c[pid] = make_float4(r.x, r.y, r.z, 0.0f);
                                 want_sh = true;
                             }
@@ -713,8 +717,8 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                                 const float maxt = sqrtf(length_sq(sd)) - (2.0f * RTG_EPS);
                                 sd = normalize(sd);
                                 const v3 so = add(x, muls(sd, RTG_EPS));
-                                p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
-                                p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, 1.0f);  // copy sh_c if visible
+                                s_sho[threadIdx.x] = make_float4(so.x, so.y, so.z, maxt);
+                                s_shd[threadIdx.x] = make_float4(sd.x, sd.y, sd.z, 1.0f);  // copy sh_c if visible
                                 p.sh_c[pid] = make_float4(r.x, r.y, r.z, 1.0f);  // .w: env sample visible
                                 want_sh = true;
                                 env_flag = 1.0f;
@@ -786,13 +790,13 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                             const v3 f = divs(alb, RTG_PI_F);  // BSDF::evaluate
                             ld = divs(muls(mul(f, emitted), g), pmf * pdf);
                             const v3 cvis = mul(thr, ld);
-                            p.sh_o[pid] = make_float4(so.x, so.y, so.z, maxt);
+                            s_sho[threadIdx.x] = make_float4(so.x, so.y, so.z, maxt);
                             // Visible is the common case: contrib takes thr * Ld now and k_trace
                             // writes thr * 0 = +0 on occlusion. When thr * 0 is not +0 (a non-finite
                             // throughput) the value goes through sh_c and is copied on visibility.
                             const v3 z = mul(thr, mk(0.0f, 0.0f, 0.0f));
                             const bool plain = (__float_as_uint(z.x) | __float_as_uint(z.y) | __float_as_uint(z.z)) == 0u;
-                            p.sh_d[pid] = make_float4(sd.x, sd.y, sd.z, plain ? 0.0f : 1.0f);
+                            s_shd[threadIdx.x] = make_float4(sd.x, sd.y, sd.z, plain ? 0.0f : 1.0f);
                             if (!plain) p.sh_c[pid] = make_float4(cvis.x, cvis.y, cvis.z, 0.0f);
                             ld_pre = plain;
                             cpre = cvis;
@@ -858,7 +862,12 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             out_t[j] = n_t;
             out_r[j] = n_r;
         }
-        if (want_sh) p.shq[os + prefix_lt(ms)] = (unsigned)pid;
+        if (want_sh) {
+            const unsigned j = os + prefix_lt(ms);
+            p.shq[j] = (unsigned)pid;  // k_trace writes the path's contrib entry on occlusion
+            p.sh_o[j] = s_sho[threadIdx.x];
+            p.sh_d[j] = s_shd[threadIdx.x];
+        }
         __syncthreads();
     }
 }
@@ -1779,6 +1788,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             io.sray_o = pb.sh_o;
             io.sray_d = pb.sh_d;
             io.sray_c = pb.sh_c;
+            io.spos = 1;
             io.scount = b > 0 ? &pb.ctr[b - 1].n_shadow : nullptr;
             io.contrib = b > 0 ? pb.contrib + (size_t)(b - 1) * a.P : nullptr;
             io.visible = nullptr;
