@@ -34,13 +34,17 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")  # rocprofv
 KSTATS = os.path.join(ROOT, "profiles", "r03_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
 ROOF_REPLAY = os.path.join(ROOT, "profiles", "r03_roof_replay.jsonl")  # tools/roof_replay.py (C3)
-# k_shade's algorithmic bytes (per path it shades; PATH integrator): reads queue id 4, ray_o 16,
-# ray_d 16, hit 16, throughput 16, meta 4, PCG state 8, pixel 4 and the hit triangle's shading record
-# 64; writes contrib 16 and meta 4; a continuing path also writes ray_o, ray_d, throughput 16 each,
-# PCG 8 and its queue id 4; an NEE sample writes sh_o, sh_d 16 each and its queue id 4. Scene records
-# shared by many paths (materials, lights, texels) are not counted.
-SHADE_B_PATH = 4 + 16 + 16 + 16 + 16 + 4 + 8 + 4 + 64 + 16 + 4
-SHADE_B_CONT = 16 + 16 + 16 + 8 + 4
+# k_shade's algorithmic bytes (PATH integrator; the payload travels with the queues):
+# every shaded path reads its direction 16, hit record 16, pixel 4 and, on a hit, the triangle's
+# shading record 64, and writes contrib 16 and meta 4; a path past the camera bounce also reads its
+# origin 16, throughput 16 and PCG state 8, which the previous shade wrote (16 + 16 + 16 + 8 with its
+# direction); an NEE sample writes sh_o, sh_d 16 each and the path id 4. Scene records shared by
+# many paths (materials, lights, texels) are not counted. The kernel time also holds k_generate (16 B
+# camera direction per path) and k_accumulate (reads each contrib entry 16 and meta 4 per path, the
+# film once): SHADE_B_CAM per path, and the contrib read-back in SHADE_B_PATH.
+SHADE_B_PATH = 16 + 16 + 4 + 64 + 16 + 4 + 16
+SHADE_B_CAM = 16 + 4
+SHADE_B_CONT = (16 + 16 + 8) + (16 + 16 + 16 + 8)
 SHADE_B_NEE = 16 + 16 + 4
 ROOF_TABLE_MIB = 69  # the hot scene of C3: 21 MB wide nodes + 48 MB triangle records
 HOT_BYTES_PER_TRI = 69.0  # wide nodes (~21 B per triangle on C3) + the 48-B triangle record
@@ -392,7 +396,8 @@ def main():
     # generate + shade + accumulate HIP events), and the PMC DRAM-level bytes of its launches
     shaded = ext_rays  # every closest-hit ray's result is shaded once
     cont = max(ext_rays - paths, 0)  # continuing paths = extension rays after the camera rays
-    shade_algo_bytes = shaded * SHADE_B_PATH + cont * SHADE_B_CONT + shadow_rays * SHADE_B_NEE
+    shade_algo_bytes = (shaded * SHADE_B_PATH + cont * SHADE_B_CONT + shadow_rays * SHADE_B_NEE + paths * SHADE_B_CAM
+                        + 12.0 * a.width * a.height * 2 * a.steps)
     shade_algo_gbs = shade_algo_bytes / (shade_ms / 1e3) / 1e9 if shade_ms > 0 else None
     shade_pmc = None
     if pmc:
@@ -510,9 +515,11 @@ def main():
                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": None if shade_algo_gbs is None else round(shade_algo_gbs / HBM_PEAK_GBS, 4),
                                "algorithmic_bytes_per_step": round(shade_algo_bytes / max(a.steps, 1)),
-                               "definition": "per shaded path %d B (payload reads + hit record + contrib/meta writes), "
-                                             "+%d B per continuing path, +%d B per NEE sample; scene records shared by "
-                                             "paths not counted" % (SHADE_B_PATH, SHADE_B_CONT, SHADE_B_NEE),
+                               "definition": "per shaded path %d B (direction, hit, pixel, shading record reads; contrib/meta "
+                                             "writes), +%d B per path past the camera bounce (its payload written by one "
+                                             "shade, read by the next), +%d B per NEE sample; scene records shared by "
+                                             "paths not counted; + %d B per path for k_generate / k_accumulate and the film read + write"
+                                             % (SHADE_B_PATH, SHADE_B_CONT, SHADE_B_NEE, SHADE_B_CAM),
                                "pmc": shade_pmc,
                                "pmc_source": (None if shade_pmc is None else "%s (k_shade<false>, DRAM-level bytes "
                                               "FETCH_SIZE x2 + WRITE_SIZE per launch, rocprof kernel-trace duration); "

@@ -4,6 +4,8 @@ Outputs (git-ignored, shipped to the GPU box with the source snapshot):
   raytracingrenderer_amd/lib/librth.so       host front-end (C++17, g++)         include/rth.h
   raytracingrenderer_amd/lib/librtg.so       HIP kernels + C-ABI (hipcc gfx950)  include/rtg.h
   raytracingrenderer_amd/lib/rtg_render      headless CLI (-scene -SPP -outputFilename)
+  raytracingrenderer_amd/lib/debug/librtg.so diagnostic build (RTG_DEBUG=1: per-wave clocks, fetch
+                                             capture + replay; tools/roof_replay.py, tools/wavetime.py)
   oracle/_build/liboracle_rtm.so             test-only CPU restatement, shared math
   oracle/_build/liboracle_libm.so            test-only CPU restatement, C-library math
   oracle/_build/libm_check                   test-only: include/rtg_math.h vs the host glibc
@@ -60,13 +62,15 @@ def build_host(force=False):
     return out
 
 
-def build_device(force=False):
-    os.makedirs(LIB, exist_ok=True)
-    out = os.path.join(LIB, "librtg.so")
+def build_device(force=False, debug=False):
+    d = os.path.join(LIB, "debug") if debug else LIB
+    os.makedirs(d, exist_ok=True)
+    out = os.path.join(d, "librtg.so")
     src = [os.path.join(CSRC, s) for s in DEVICE_SRC]
     if force or _newer(out, _deps(src)):
         _run([HIPCC, "--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-std=c++17",
-              "-fPIC", "-shared", "-o", out] + src + ["-ldl", "-Wl,-rpath,/opt/rocm/lib"])
+              "-fPIC", "-shared"] + (["-DRTG_DEBUG=1"] if debug else []) + ["-o", out] + src +
+             ["-ldl", "-Wl,-rpath,/opt/rocm/lib"])
     return out
 
 
@@ -132,6 +136,7 @@ def build_all(force=False, device=True):
     build_host(force)
     if device:
         build_device(force)
+        build_device(force, debug=True)
     build_cli(force)
     build_oracle(force)
     build_ref(force)

@@ -24,9 +24,22 @@ sys.path.insert(0, ROOT)
 
 def scene(a):
     from raytracingrenderer_amd import loadScene, write_synthetic_scene
+    if a.config != "C3":
+        from bench import CONFIGS, scene_dir
+        c = CONFIGS[a.config]
+        return loadScene(scene_dir(c["scene"]), width=a.width, height=a.height,
+                         skip_missing=c.get("skip_missing", False), envmap=c.get("envmap"))
     d = tempfile.mkdtemp(prefix="rtg_roof_")
     write_synthetic_scene(d, n_tris=a.tris, seed=20251015, width=a.width, height=a.height)
     return loadScene(d)
+
+
+def tiles(a):
+    """rank 0's tiles of a frame split over --shard-of ranks (None: the whole frame)."""
+    if a.shard_of <= 1:
+        return None
+    from raytracingrenderer_amd.distributed import tiles_for_rank
+    return tiles_for_rank(a.width, a.height, 0, a.shard_of)
 
 
 def product(a):
@@ -34,14 +47,15 @@ def product(a):
     from raytracingrenderer_amd import RayTracer
     from raytracingrenderer_amd import _native as N
     s = scene(a)
+    tl = tiles(a)
     rt = RayTracer(s, max_depth=a.max_depth, seed=1234)
     rt.set_options(flags=N.RTG_OPT_CULL)
-    rt.render(a.spp, first_sample=0)  # warm-up
+    rt.render(a.spp, tiles=tl, first_sample=0)  # warm-up
     best = None
     for _ in range(a.reps):
         rt.clear()
         rt.set_options(flags=N.RTG_OPT_CULL | N.RTG_OPT_TIMING)
-        rt.render(a.spp, first_sample=0)
+        rt.render(a.spp, tiles=tl, first_sample=0)
         n = C.c_uint32()
         ms = (C.c_double * 64)()
         N.rtg().rtg_launch_times(rt._h, ms, 64, C.byref(n))
@@ -49,7 +63,7 @@ def product(a):
         best = t if best is None else [min(x, y) for x, y in zip(best, t)]
     rt.clear()
     rt.set_options(flags=N.RTG_OPT_CULL | N.RTG_OPT_COUNT)
-    rt.render(a.spp, first_sample=0)
+    rt.render(a.spp, tiles=tl, first_sample=0)
     st = rt.stats()
     fetches = st["node_lane_steps"] + st["tri_tests"] + st["shadow_tri_tests"] + st["leafbox_tests"]
     print(json.dumps({"launch_ms": best, "count_fetches": fetches,
@@ -60,13 +74,14 @@ def replay(a):
     from raytracingrenderer_amd import RayTracer
     from raytracingrenderer_amd import _native as N
     s = scene(a)
+    tl = tiles(a)
     rt = RayTracer(s, max_depth=a.max_depth, seed=1234)
     rt.set_options(flags=N.RTG_OPT_CULL)
     L = N.rtg()
     for b in range(a.max_depth + 3):
         rt.clear()
         assert L.rtg_debug_capture(rt._h, b) == 0, L.rtg_last_error()
-        rt.render(a.spp, first_sample=0)
+        rt.render(a.spp, tiles=tl, first_sample=0)
         out = (C.c_double * 4)()
         assert L.rtg_debug_replay(rt._h, out) == 0, L.rtg_last_error()
         print(json.dumps({"launch": b, "replay_ms": out[0], "replayed_fetches": out[1],
@@ -78,19 +93,27 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--lib", default=os.path.join(ROOT, "raytracingrenderer_amd", "lib", "debug", "librtg.so"))
     p.add_argument("--mode", default="all", choices=["all", "product", "replay"])
+    p.add_argument("--config", default="C3", help="a bench.py config (scene, size, spp, depth)")
     p.add_argument("--tris", type=int, default=1_000_000)
-    p.add_argument("--width", type=int, default=1024)
-    p.add_argument("--height", type=int, default=1024)
-    p.add_argument("--spp", type=int, default=64)
-    p.add_argument("--max-depth", type=int, default=4)
+    p.add_argument("--width", type=int, default=0)
+    p.add_argument("--height", type=int, default=0)
+    p.add_argument("--spp", type=int, default=0)
+    p.add_argument("--max-depth", type=int, default=0)
     p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--shard-of", type=int, default=1, help="rank 0's tiles of an N-way split (bench --shard-of)")
     a = p.parse_args()
+    from bench import CONFIGS
+    c = CONFIGS[a.config]
+    a.width = a.width or c["width"]
+    a.height = a.height or c["height"]
+    a.spp = a.spp or c["spp"]
+    a.max_depth = a.max_depth or c["depth"]
     if a.mode == "product":
         return product(a)
     if a.mode == "replay":
         return replay(a)
-    base = [sys.executable, os.path.abspath(__file__), "--tris", str(a.tris), "--width", str(a.width), "--height",
-            str(a.height), "--spp", str(a.spp), "--max-depth", str(a.max_depth), "--reps", str(a.reps)]
+    base = [sys.executable, os.path.abspath(__file__), "--config", a.config, "--tris", str(a.tris), "--width", str(a.width), "--height",
+            str(a.height), "--spp", str(a.spp), "--max-depth", str(a.max_depth), "--reps", str(a.reps), "--shard-of", str(a.shard_of)]
     env = dict(os.environ)
     env.pop("RTG_LIB", None)
     prod = subprocess.run(base + ["--mode", "product"], capture_output=True, text=True, env=env, timeout=900)
