@@ -17,12 +17,16 @@ using namespace rtgd;
 #define RTG_POP ((int)0x80000001)  // "pop the stack" marker inside one traversal step
 // Measured constants of the traversal and shading kernels (DESIGN.md §4 records the A/B runs;
 // the rejected alternatives are archived under tools/experiments/, not compiled in):
+#ifndef RTG_STACK
 #define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (24 KB per block)
+#endif
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
 #define RTG_REFILL 12       // refill idle lanes once at least this many are idle (the setup code then
                             // runs with more lanes per execution)
+#ifndef RTG_TRACE_WPE
 #define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel (80 VGPRs)
+#endif
 #define RTG_CULL_REL 1.52587890625e-05f  // 2^-16 relative inflation for distance culling
 #define RTG_FETCH 256       // rays a wave takes from a work counter per atomic (k_trace pool)
 #define RTG_FETCH_TAIL 8    // fetch RTG_TAIL_BATCH rays per atomic once about this many rounds of
@@ -48,8 +52,7 @@ struct __align__(16) Counters {
 };
 #undef RTG_CPAD
 
-// Queues hold path ids only; ray payloads live in per-path arrays (written in place by k_shade),
-// so compaction moves 4 bytes per ray and needs one atomic per 256 paths.
+// A ray's payload sits at its queue position (PathBufs); compaction needs one atomic per 256 paths.
 // One traversal launch serves two ray sets: extension (closest-hit) rays take work indices
 // [0, nc) and NEE shadow (any-hit) rays [nc, nc + ns). Each lane carries its ray's kind.
 struct TraceIO {
