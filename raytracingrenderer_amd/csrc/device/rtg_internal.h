@@ -32,7 +32,7 @@ using namespace rtgd;
 #define RTG_FETCH_TAIL 8    // fetch RTG_TAIL_BATCH rays per atomic once about this many rounds of
 #define RTG_TAIL_BATCH 64   // big batches are left in the slice (shorter drain tails)
 #ifndef RTG_SHADE_WAVES
-#define RTG_SHADE_WAVES 5   // min waves per SIMD for k_shade (96 VGPRs, no spills)
+#define RTG_SHADE_WAVES 7   // min waves per SIMD for k_shade (72 VGPRs, no spills; one tile per block)
 #endif
 // RTG_DEBUG=1 (a diagnostic build only) compiles k_trace's per-wave clocks (RTG_OPT_WAVETIME) and
 // the fetch capture + replay of the locality-matched roofline (RTG_OPT_CAPTURE, rtg_debug_replay).
@@ -49,8 +49,17 @@ struct __align__(16) Counters {
     RTG_CPAD(n_ext) RTG_CPAD(n_shadow) RTG_CPAD(f_ext) RTG_CPAD(f_shadow) RTG_CPAD(f_shade) RTG_CPAD(pad0)
     RTG_CPAD(pad1) RTG_CPAD(pad2)
     unsigned f8[8 * 32];  // sliced work counters of k_trace (TraceIO::fetch8), one 128-B line each
+    // path tracer queues, segmented: k_shade block t appends to segment t % 8 (a device-scope atomic
+    // on one counter serialises at ~87M/s: one counter for all blocks made k_shade atomic-bound,
+    // tools/micro/atomic.hip); segment k holds ne8[32k] extension / ns8[32k] shadow rays from
+    // queue position k * seg_cap (ChunkArgs::seg_cap), and is k_trace's slice k
+    unsigned ne8[8 * 32];
+    unsigned ns8[8 * 32];
 };
 #undef RTG_CPAD
+// positions of a segmented queue for P paths: 8 segments of ceil(ceil(P / 256) / 8) tiles of 256
+static inline size_t seg_tiles(size_t P) { return ((P + 255) / 256 + 7) / 8; }
+static inline size_t queue_slots(size_t P) { return seg_tiles(P) * 8 * 256; }
 
 // A ray's payload sits at its queue position (PathBufs); compaction needs one atomic per 256 paths.
 // One traversal launch serves two ray sets: extension (closest-hit) rays take work indices
@@ -73,6 +82,12 @@ struct TraceIO {
     int* visible;              // any-hit query output [pid] (instead of contrib)
     unsigned* fetch;           // work counter over both sets (device, zeroed)
     unsigned* fetch8;          // or (non-null) 8 slice counters at a stride of 32 (device, zeroed)
+    unsigned seg_cap;          // != 0: segmented queues (path tracer, bounce >= 1): slice k = the
+                               // seg_ne[32k] extension rays at positions k * seg_cap.. then the
+                               // seg_ns[32k] shadow rays at shadow positions k * seg_cap..; the
+                               // extension index span `count` is then 8 * seg_cap
+    const unsigned* seg_ne;    // (null: no extension rays)
+    const unsigned* seg_ns;    // (null: no shadow rays)
     int* ovf;                  // global stack overflow [level][thread]
     unsigned long long* stats; // [0,1] closest / [4,5] any-hit: box tests, triangle tests (COUNT)
     int cull;
@@ -96,6 +111,7 @@ struct ChunkArgs {
     DevCamera cam;
     int lean = 0;              // 1: bounce-0 state implied (identity queue, camera origin, thr 1,
                                // PCG seed, canHitLight); k_generate writes ray_d only
+    unsigned seg_tiles = 0;    // tiles of 256 per queue segment (Counters::ne8); k_shade grid = 8x
     // path ids are pixel-major: pid = lp * ns + sl (a wave of camera rays is one pixel's samples)
 };
 

@@ -38,6 +38,24 @@
 // queue (one atomic per 64 rays) into a wave-uniform pool, and every lane whose ray terminates
 // immediately takes the next index from the pool. Without replacement a wave runs until its
 // longest ray finishes (measured SIMD efficiency ~27 %).
+// Work slice k of a trace launch. Path tracer (segmented queues, io.seg_cap != 0; io.fetch8: one
+// counter per slice, by blockIdx % 8, i.e. one per XCD): slice k is queue segment k, its extension
+// rays at positions [k * seg_cap, + elen) and then its shadow rays at the same shadow positions, so
+// every XCD walks long closest-hit rays first and ends on any-hit rays; len rays in all. Otherwise
+// (one counter: light tracer, ray queries): every ray, extension rays first.
+static __device__ __forceinline__ void trace_slice(const TraceIO& io, unsigned nc, unsigned n, int k, unsigned& elo,
+                                                   unsigned& elen, unsigned& len) {
+    if (io.seg_cap) {
+        elo = (unsigned)k * io.seg_cap;
+        elen = io.seg_ne ? io.seg_ne[32 * k] : 0u;
+        len = elen + (io.seg_ns ? io.seg_ns[32 * k] : 0u);
+    } else {
+        elo = 0;
+        elen = nc;
+        len = n;
+    }
+}
+
 template <bool COUNT>
 __global__ __launch_bounds__(RTG_TB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
 void k_trace(SceneView s, TraceIO io) {
@@ -47,23 +65,27 @@ void k_trace(SceneView s, TraceIO io) {
     const int lane = lane_id();
     const unsigned gthreads = gridDim.x * blockDim.x;
     const unsigned gtid = blockIdx.x * blockDim.x + tid;
-    const unsigned nc = io.count ? *io.count : 0u;
+    // extension index span: the ray count, or (segmented queues) all 8 segments' positions
+    const unsigned nc = io.seg_cap ? 8u * io.seg_cap : (io.count ? *io.count : 0u);
     const unsigned n = nc + (io.scount ? *io.scount : 0u);
     unsigned long long c_nodes = 0, c_tris = 0, c_snodes = 0, c_stris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0,
                        c_cullpop = 0, c_pops = 0, c_lslots = 0, c_lbox = 0;
     unsigned c_tails = 0;  // triangle records whose last 16 B were fetched (COUNT)
     unsigned pool_base = 0, pool_left = 0, last_b = 0;  // wave-uniform
     const unsigned tail_rays = (gthreads / 64u) * (unsigned)RTG_FETCH * RTG_FETCH_TAIL / (io.fetch8 ? 8u : 1u);
-    const unsigned ns = n - nc;
-    // io.fetch8: 8 work slices (one counter each, by blockIdx % 8: one per XCD). Slice k holds the
-    // k-th eighth of the extension rays followed by the k-th eighth of the shadow rays, so every XCD
-    // walks long closest-hit rays first and ends on any-hit rays.
-    auto slice_lo = [&](int k) {
-        return !io.fetch8 ? 0u
-                          : (unsigned)(((unsigned long long)nc * (unsigned)k) >> 3) + (unsigned)(((unsigned long long)ns * (unsigned)k) >> 3);
-    };
+    // the 8 slices (trace_slice) in LDS, read when a wave fetches work: the loop keeps only the
+    // slice number in a register
+    __shared__ unsigned s_tab[3][8];
+    if (tid < 8) {
+        unsigned elo, elen, len;
+        trace_slice(io, nc, n, tid, elo, elen, len);
+        s_tab[0][tid] = elo;
+        s_tab[1][tid] = elen;
+        s_tab[2][tid] = len;
+    }
+    __syncthreads();
     int slice = io.fetch8 ? (int)(blockIdx.x & 7u) : 0, tried = 0;  // wave-uniform
-    unsigned s_lo = slice_lo(slice), s_len = (io.fetch8 ? slice_lo(slice + 1) : n) - s_lo;
+    unsigned s_len = __builtin_amdgcn_readfirstlane(s_tab[2][slice]);
     bool drained = false;                   // wave-uniform
     bool have = false;
     unsigned ri = 0;
@@ -122,7 +144,7 @@ void k_trace(SceneView s, TraceIO io) {
                 b = __builtin_amdgcn_readfirstlane(b);  // wave-uniform: keeps the fetch state in SGPRs
                 last_b = b;
                 if (b < s_len) {
-                    pool_base = s_lo + b;
+                    pool_base = b;
                     pool_left = min(g, s_len - b);
                 } else if (!io.fetch8 || ++tried == 8) {
                     drained = true;
@@ -130,8 +152,7 @@ void k_trace(SceneView s, TraceIO io) {
                     break;
                 } else {
                     slice = (slice + 1) & 7;
-                    s_lo = slice_lo(slice);
-                    s_len = slice_lo(slice + 1) - s_lo;
+                    s_len = __builtin_amdgcn_readfirstlane(s_tab[2][slice]);
                     last_b = s_len;  // a stolen slice is near its end: small batches
                 }
             }
@@ -139,13 +160,9 @@ void k_trace(SceneView s, TraceIO io) {
                 const unsigned pos = prefix_lt(im);
                 const unsigned take = min((unsigned)__popcll(im), pool_left);
                 if (!have && pos < take) {
-                    ri = pool_base + pos;
-                    if (io.fetch8) {
-                        const unsigned e_lo = (unsigned)(((unsigned long long)nc * (unsigned)slice) >> 3);
-                        const unsigned e_len = (unsigned)(((unsigned long long)nc * (unsigned)(slice + 1)) >> 3) - e_lo;
-                        const unsigned j = ri - s_lo;
-                        ri = j < e_len ? e_lo + j : nc + (unsigned)(((unsigned long long)ns * (unsigned)slice) >> 3) + (j - e_len);
-                    }
+                    const unsigned j = pool_base + pos;  // index within the slice
+                    const unsigned s_elo = s_tab[0][slice], s_elen = s_tab[1][slice];
+                    ri = j < s_elen ? s_elo + j : nc + s_elo + (j - s_elen);
                     have = true;
                     if (RTG_DEBUG) { cap_ri = ri; cap_k = 0; }
                     anyr = ri >= nc;
@@ -426,6 +443,28 @@ void k_trace(SceneView s, TraceIO io) {
     }
 }
 
+// The slice table of the captured launch (trace_slice for k = 0..7: elo, elen, slo, shadow count at
+// [k], [8 + k], [16 + k], [24 + k]; [32] the extension index span, [33] / [34] the ray counts).
+__global__ void k_cap_slices(TraceIO io, unsigned* tab) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const unsigned nc = io.seg_cap ? 8u * io.seg_cap : (io.count ? *io.count : 0u);
+    const unsigned n = nc + (io.scount ? *io.scount : 0u);
+    unsigned te = 0, ts = 0;
+    for (int k = 0; k < 8; ++k) {
+        unsigned elo, elen, len;
+        trace_slice(io, nc, n, k, elo, elen, len);
+        tab[k] = elo;
+        tab[8 + k] = elen;
+        tab[16 + k] = elo;
+        tab[24 + k] = len - elen;
+        te += elen;
+        ts += len - elen;
+    }
+    tab[32] = nc;
+    tab[33] = te;
+    tab[34] = ts;
+}
+
 #if RTG_DEBUG
 // ------------------------------------------------------------------ locality-matched ceiling
 // Replays the record fetches k_trace made for every ray of one launch (captured in order by
@@ -437,13 +476,13 @@ void k_trace(SceneView s, TraceIO io) {
 // every ray is one dependent chain, as in the walk. Its time is the memory system's time for this
 // exact access stream: the ceiling k_trace's time is compared against.
 __global__ __launch_bounds__(RTG_TB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
-void k_replay(SceneView s, const uint4* cap, const unsigned* cap_len, unsigned n, unsigned cap_n, unsigned zero,
-              unsigned* fetch8, unsigned long long* total, float* out) {
+void k_replay(SceneView s, const uint4* cap, const unsigned* cap_len, const unsigned* tab, unsigned cap_n,
+              unsigned zero, unsigned* fetch8, unsigned long long* total, float* out) {
     const int lane = lane_id();
     const int slice0 = (int)(blockIdx.x & 7u);
     int slice = slice0, tried = 0;
-    auto slo = [&](int k) { return (unsigned)(((unsigned long long)n * (unsigned)k) >> 3); };
-    unsigned s_lo = slo(slice), s_len = slo(slice + 1) - s_lo;
+    const unsigned nc = tab[32];
+    unsigned s_elo = tab[slice], s_elen = tab[8 + slice], s_slo = tab[16 + slice], s_len = s_elen + tab[24 + slice];
     unsigned pool_base = 0, pool_left = 0;
     bool drained = false, have = false;
     unsigned ri = 0, k = 0, len = 0, dep = 0;
@@ -458,23 +497,26 @@ void k_replay(SceneView s, const uint4* cap, const unsigned* cap_len, unsigned n
                 if (lane == 0) b = atomicAdd(fetch8 + 32 * slice, 64u);
                 b = __builtin_amdgcn_readfirstlane(b);
                 if (b < s_len) {
-                    pool_base = s_lo + b;
+                    pool_base = b;
                     pool_left = min(64u, s_len - b);
                 } else if (++tried == 8) {
                     drained = true;
                     break;
                 } else {
                     slice = (slice + 1) & 7;
-                    s_lo = slo(slice);
-                    s_len = slo(slice + 1) - s_lo;
+                    s_elo = tab[slice];
+                    s_elen = tab[8 + slice];
+                    s_slo = tab[16 + slice];
+                    s_len = s_elen + tab[24 + slice];
                 }
             }
             if (pool_left > 0) {
                 const unsigned pos = prefix_lt(im);
                 const unsigned take = min((unsigned)__popcll(im), pool_left);
                 if (!have && pos < take) {
-                    ri = pool_base + pos;
-                    len = min(cap_len[ri], (unsigned)RTG_CAP_LEN);
+                    const unsigned j = pool_base + pos;
+                    ri = j < s_elen ? s_elo + j : nc + s_slo + (j - s_elen);
+                    len = ri < cap_n ? min(cap_len[ri], (unsigned)RTG_CAP_LEN) : 0u;
                     k = 0;
                     have = len > 0;
                 }
@@ -520,7 +562,11 @@ void k_replay(SceneView s, const uint4* cap, const unsigned* cap_len, unsigned n
 // ------------------------------------------------------------------ generate
 __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
     const unsigned pid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (pid == 0) p.ctr[0].n_ext = a.P;
+    if (a.seg_tiles && pid < 8) {  // path tracer: the camera rays as queue segments (positions = path ids)
+        const unsigned cap = a.seg_tiles * RTG_TB, lo = pid * cap;
+        p.ctr[0].ne8[32 * pid] = a.P > lo ? min(cap, a.P - lo) : 0u;
+    }
+    if (!a.seg_tiles && pid == 0) p.ctr[0].n_ext = a.P;  // instant radiosity's camera pass: one queue
     if (pid >= a.P) return;
     const unsigned lp = pid / a.ns, sl = pid % a.ns;  // pixel-major path ids
     const unsigned pixel = a.pixlist[lp];
@@ -569,7 +615,16 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     const bool lean0 = b == 0;  // bounce 0: path id = position, camera origin, thr 1, PCG seed, canHitLight
-    const unsigned n = lean0 ? a.P : p.ctr[b].n_ext;
+    // This block's tile of 256 queue positions [base, base + 256), live below n: tile blockIdx / 8
+    // of input segment blockIdx % 8 (Counters::ne8; bounce 0: the camera rays, positions = path
+    // ids). Its continuing paths and NEE rays are appended to the same segment of the next queues:
+    // a segment keeps its region of the image from bounce to bounce (it is k_trace's slice k, walked
+    // by XCD k), and blocks running together append to 8 different counters.
+    const unsigned cap = a.seg_tiles * RTG_TB;
+    const unsigned sg = blockIdx.x & 7u;
+    const unsigned base = sg * cap + (blockIdx.x >> 3) * RTG_TB;
+    const unsigned n = sg * cap + p.ctr[b].ne8[32 * sg];
+    if (base >= n) return;  // block-uniform
     // extension payload of this bounce (set b & 1, by queue position) and of the next (set (b+1) & 1)
     const float4* in_o = (b & 1) ? p.ray_o2 : p.ray_o;
     const float4* in_d = (b & 1) ? p.ray_d2 : p.ray_d;
@@ -580,9 +635,8 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
     float4* out_t = (b & 1) ? p.thr : p.thr2;
     unsigned long long* out_r = (b & 1) ? p.rng : p.rng2;
     float4* contrib = p.contrib + (size_t)b * a.P;
-    // block-uniform loop: all waves of a block take part in every compaction round (the launch has
-    // one 256-path tile per block: a finished block frees its slot for the next tile)
-    for (unsigned base = blockIdx.x * RTG_TB; base < n; base += gridDim.x * RTG_TB) {
+    // one 256-path tile per block: a finished block frees its slot for the next tile
+    {
         const unsigned i = base + threadIdx.x;
         int pid = 0;
         bool want_ext = false, want_sh = false;
@@ -846,8 +900,9 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                 te += s_cnt[0][w];
                 ts += s_cnt[1][w];
             }
-            s_base[0] = te ? atomicAdd(&p.ctr[b + 1].n_ext, te) : 0u;
-            s_base[1] = ts ? atomicAdd(&p.ctr[b].n_shadow, ts) : 0u;
+            // (at most seg_tiles blocks append to a segment: it cannot overflow)
+            s_base[0] = te ? atomicAdd(&p.ctr[b + 1].ne8[32 * sg], te) + sg * cap : 0u;
+            s_base[1] = ts ? atomicAdd(&p.ctr[b].ns8[32 * sg], ts) + sg * cap : 0u;
         }
         __syncthreads();
         unsigned oe = s_base[0], os = s_base[1];
@@ -986,6 +1041,10 @@ __global__ void k_tally(const Counters* ctr, int maxb, unsigned long long* stats
     for (int b = 0; b < maxb; ++b) {
         e += ctr[b].n_ext;
         sh += ctr[b].n_shadow;
+        for (int k = 0; k < 8; ++k) {  // segmented queues (path tracer)
+            e += ctr[b].ne8[32 * k];
+            sh += ctr[b].ns8[32 * k];
+        }
     }
     atomicAdd(&stats[2], e);  // chunk pipelines may tally concurrently
     atomicAdd(&stats[3], sh);
@@ -1009,22 +1068,23 @@ int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
     if (P <= h->cap_P && maxb <= h->cap_maxb) return RTG_OK;
     free_chunk(h);
     PathBufs& p = h->pb;
-    HIPOK(hipMalloc((void**)&p.thr, P * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.rng, P * sizeof(unsigned long long)));
+    const size_t Q = queue_slots(P);  // arrays indexed by queue position (segmented queues)
+    HIPOK(hipMalloc((void**)&p.thr, Q * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.rng, Q * sizeof(unsigned long long)));
     HIPOK(hipMalloc((void**)&p.meta, P * sizeof(int)));
     HIPOK(hipMalloc((void**)&p.contrib, P * (size_t)maxb * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.q[0], P * sizeof(unsigned)));
     HIPOK(hipMalloc((void**)&p.q[1], P * sizeof(unsigned)));
-    HIPOK(hipMalloc((void**)&p.shq, P * sizeof(unsigned)));
-    HIPOK(hipMalloc((void**)&p.hits, P * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.ray_o, P * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.ray_d, P * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.thr2, P * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.rng2, P * sizeof(unsigned long long)));
-    HIPOK(hipMalloc((void**)&p.ray_o2, P * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.ray_d2, P * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.sh_o, P * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.sh_d, P * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.shq, Q * sizeof(unsigned)));
+    HIPOK(hipMalloc((void**)&p.hits, Q * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.ray_o, Q * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.ray_d, Q * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.thr2, Q * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.rng2, Q * sizeof(unsigned long long)));
+    HIPOK(hipMalloc((void**)&p.ray_o2, Q * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.ray_d2, Q * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.sh_o, Q * sizeof(float4)));
+    HIPOK(hipMalloc((void**)&p.sh_d, Q * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.sh_c, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.ctr, (size_t)(maxb + 1) * sizeof(Counters)));
     h->cap_P = P;
@@ -1757,6 +1817,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         a.mode = h->integrator;
         a.cam = h->cam;
         a.lean = 1;
+        a.seg_tiles = (unsigned)seg_tiles(a.P);
         HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), st));
         timed_begin(h, st, k);
         hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, pb);
@@ -1768,7 +1829,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             if (b > 0) {
                 // one 256-path tile per block (blocks past the live count exit at once)
                 timed_begin(h, st, k);
-                const unsigned sgrid = (unsigned)((a.P + RTG_TB - 1) / RTG_TB);
+                const unsigned sgrid = 8u * a.seg_tiles;  // >= P / 256: every tile of every segment
                 if (h->integrator == RTG_INTEGRATOR_PATH)
                     hipLaunchKernelGGL(k_shade<false>, dim3(sgrid), dim3(RTG_TB), 0, st, h->sv, a, pb, b - 1);
                 else
@@ -1782,14 +1843,18 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             io.ray_o = b == 0 ? nullptr : ((b & 1) ? pb.ray_o2 : pb.ray_o);
             io.cam_o = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f);
             io.ray_d = (b & 1) ? pb.ray_d2 : pb.ray_d;
-            io.count = b < maxb ? &pb.ctr[b].n_ext : nullptr;
+            // segmented queues (bounce 0: the P camera rays at identity positions, cut by k_generate)
+            io.count = nullptr;
+            io.seg_cap = a.seg_tiles * RTG_TB;
+            io.seg_ne = b < maxb ? pb.ctr[b].ne8 : nullptr;
+            io.seg_ns = b > 0 ? pb.ctr[b - 1].ns8 : nullptr;
             io.hits = pb.hits;
             io.squeue = pb.shq;
             io.sray_o = pb.sh_o;
             io.sray_d = pb.sh_d;
             io.sray_c = pb.sh_c;
             io.spos = 1;
-            io.scount = b > 0 ? &pb.ctr[b - 1].n_shadow : nullptr;
+            io.scount = nullptr;
             io.contrib = b > 0 ? pb.contrib + (size_t)(b - 1) * a.P : nullptr;
             io.visible = nullptr;
             io.fetch = &pb.ctr[b].f_ext;
@@ -1798,18 +1863,17 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             io.cap = nullptr;
             io.cap_len = nullptr;
             if (RTG_DEBUG && c == 0 && b == h->capture_launch) {
-                const size_t cn = (size_t)a.P * (b == 0 ? 1 : 2);
+                const size_t cn = 2 * (size_t)a.seg_tiles * 8 * RTG_TB;  // both index spans
                 (void)hipFree(h->d_cap);
                 (void)hipFree(h->d_cap_len);
                 h->d_cap = nullptr;
                 h->d_cap_len = nullptr;
                 HIPOK(hipMalloc((void**)&h->d_cap, cn * (RTG_CAP_LEN / 4) * sizeof(uint4)));
                 HIPOK(hipMalloc((void**)&h->d_cap_len, cn * sizeof(unsigned)));
-                if (!h->d_cap_rays) HIPOK(hipMalloc((void**)&h->d_cap_rays, 2 * sizeof(unsigned)));
+                if (!h->d_cap_rays) HIPOK(hipMalloc((void**)&h->d_cap_rays, 35 * sizeof(unsigned)));
                 HIPOK(hipMemsetAsync(h->d_cap_len, 0, cn * sizeof(unsigned), st));
-                HIPOK(hipMemsetAsync(h->d_cap_rays, 0, 2 * sizeof(unsigned), st));
-                if (io.count) HIPOK(hipMemcpyAsync(h->d_cap_rays, io.count, 4, hipMemcpyDeviceToDevice, st));
-                if (io.scount) HIPOK(hipMemcpyAsync(h->d_cap_rays + 1, io.scount, 4, hipMemcpyDeviceToDevice, st));
+                hipLaunchKernelGGL(k_cap_slices, dim3(1), dim3(64), 0, st, io, h->d_cap_rays);
+                LAUNCH_OK("k_cap_slices");
                 h->cap_n = (unsigned)cn;
                 io.cap = h->d_cap;
                 io.cap_len = h->d_cap_len;
@@ -2012,9 +2076,9 @@ int rtg_debug_replay(rtg_handle* h, double* out) {
     if (!h->d_cap) { g_err = "rtg_debug_replay: nothing captured"; return RTG_ERR_ARG; }
     HIPOK(hipSetDevice(h->device));
     HIPOK(hipStreamSynchronize(h->stream));
-    unsigned rays[2] = {0, 0};
-    HIPOK(hipMemcpy(rays, h->d_cap_rays, sizeof(rays), hipMemcpyDeviceToHost));
-    const unsigned n = rays[0] + rays[1];
+    unsigned tab[35];
+    HIPOK(hipMemcpy(tab, h->d_cap_rays, sizeof(tab), hipMemcpyDeviceToHost));
+    const unsigned rays[2] = {tab[33], tab[34]};
     unsigned* d_f8 = nullptr;
     unsigned long long* d_tot = nullptr;
     float* d_out = nullptr;
@@ -2031,7 +2095,8 @@ int rtg_debug_replay(rtg_handle* h, double* out) {
         HIPOK(hipMemsetAsync(d_tot, 0, sizeof(unsigned long long), h->stream));
         HIPOK(hipEventRecord(e0, h->stream));
         hipLaunchKernelGGL(k_replay, dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, (const uint4*)h->d_cap,
-                           (const unsigned*)h->d_cap_len, n, h->cap_n, 0u, d_f8, d_tot, d_out);
+                           (const unsigned*)h->d_cap_len, (const unsigned*)h->d_cap_rays, h->cap_n, 0u, d_f8, d_tot,
+                           d_out);
         LAUNCH_OK("k_replay");
         HIPOK(hipEventRecord(e1, h->stream));
         HIPOK(hipEventSynchronize(e1));
