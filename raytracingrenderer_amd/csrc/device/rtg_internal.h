@@ -223,6 +223,14 @@ struct rtg_handle {
     rtg_stats stats{};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> kev;  // per-launch timing events (timing mode)
+    // k_shade's grid: the segment counts of every bounce's extension queue read back (pinned, one
+    // 1-KB Counters::ne8 block per bounce) while the next traversal runs, so the launch covers the
+    // live tiles only
+    unsigned* h_cnt = nullptr;
+    int cap_cnt = 0;
+    std::vector<hipEvent_t> cev;  // [b]: bounce b's counts are in h_cnt (on cstream)
+    std::vector<hipEvent_t> sev;  // [b]: k_shade producing them has finished (on the render stream)
+    hipStream_t cstream = nullptr;  // the read-backs, off the render stream
 };
 
 

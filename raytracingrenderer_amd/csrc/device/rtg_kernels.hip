@@ -1663,6 +1663,10 @@ void rtg_destroy(rtg_handle* h) {
     (void)hipFree(h->d_pix); (void)hipFree(h->d_ovf); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
     for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : h->kev) (void)hipEventDestroy(e);
+    for (auto& e : h->cev) (void)hipEventDestroy(e);
+    for (auto& e : h->sev) (void)hipEventDestroy(e);
+    if (h->cstream) (void)hipStreamDestroy(h->cstream);
+    if (h->h_cnt) (void)hipHostFree(h->h_cnt);
     (void)hipFree(h->d_cap); (void)hipFree(h->d_cap_len); (void)hipFree(h->d_cap_rays);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -1804,6 +1808,21 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         HIPOK(hipMalloc((void**)&d_wt, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long)));
         HIPOK(hipMemsetAsync(d_wt, 0, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long), st));
     }
+    if (h->cap_cnt < maxb + 1) {
+        if (h->h_cnt) (void)hipHostFree(h->h_cnt);
+        h->h_cnt = nullptr;
+        h->cap_cnt = 0;
+        HIPOK(hipHostMalloc((void**)&h->h_cnt, (size_t)(maxb + 1) * 256 * sizeof(unsigned), hipHostMallocDefault));
+        h->cap_cnt = maxb + 1;
+    }
+    while ((int)h->cev.size() < maxb + 1) {
+        hipEvent_t e, f;
+        HIPOK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        h->cev.push_back(e);
+        HIPOK(hipEventCreateWithFlags(&f, hipEventDisableTiming));
+        h->sev.push_back(f);
+    }
+    if (!h->cstream) HIPOK(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
     uint32_t c = 0;
     for (uint32_t s0 = first; s0 < first + n_samples; s0 += ns_chunk, ++c) {
         ChunkArgs a;
@@ -1827,15 +1846,36 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         // or generate) and the shadow rays of bounce b-1: one persistent launch, one drain tail.
         for (int b = 0; b <= maxb; ++b) {
             if (b > 0) {
-                // one 256-path tile per block (blocks past the live count exit at once)
-                timed_begin(h, st, k);
-                const unsigned sgrid = 8u * a.seg_tiles;  // >= P / 256: every tile of every segment
-                if (h->integrator == RTG_INTEGRATOR_PATH)
-                    hipLaunchKernelGGL(k_shade<false>, dim3(sgrid), dim3(RTG_TB), 0, st, h->sv, a, pb, b - 1);
-                else
-                    hipLaunchKernelGGL(k_shade<true>, dim3(sgrid), dim3(RTG_TB), 0, st, h->sv, a, pb, b - 1);
-                LAUNCH_OK("k_shade");
-                timed_end(h, st, k); kinds.push_back(2); ++k;
+                // one 256-path tile per block: 8 x the largest segment's live tiles (the segment
+                // counts of bounce b - 1 arrived while k_trace(b - 1) ran; bounce 0: the camera rays)
+                unsigned tiles = 0;
+                const unsigned cap = a.seg_tiles * RTG_TB;
+                for (int sgm = 0; sgm < 8; ++sgm) {
+                    unsigned live = 0;
+                    if (b == 1) {
+                        live = a.P > sgm * cap ? std::min(cap, a.P - sgm * cap) : 0u;
+                    } else {
+                        if (sgm == 0) HIPOK(hipEventSynchronize(h->cev[b - 1]));
+                        live = h->h_cnt[256 * (b - 1) + 32 * sgm];
+                    }
+                    tiles = std::max(tiles, (live + RTG_TB - 1) / RTG_TB);
+                }
+                if (tiles) {
+                    timed_begin(h, st, k);
+                    if (h->integrator == RTG_INTEGRATOR_PATH)
+                        hipLaunchKernelGGL(k_shade<false>, dim3(8 * tiles), dim3(RTG_TB), 0, st, h->sv, a, pb, b - 1);
+                    else
+                        hipLaunchKernelGGL(k_shade<true>, dim3(8 * tiles), dim3(RTG_TB), 0, st, h->sv, a, pb, b - 1);
+                    LAUNCH_OK("k_shade");
+                    timed_end(h, st, k); kinds.push_back(2); ++k;
+                }
+                if (b < maxb) {  // the next bounce's segment counts, for its k_shade grid
+                    HIPOK(hipEventRecord(h->sev[b], st));
+                    HIPOK(hipStreamWaitEvent(h->cstream, h->sev[b], 0));
+                    HIPOK(hipMemcpyAsync(h->h_cnt + 256 * b, pb.ctr[b].ne8, 256 * sizeof(unsigned),
+                                         hipMemcpyDeviceToHost, h->cstream));
+                    HIPOK(hipEventRecord(h->cev[b], h->cstream));
+                }
             }
             // extension payload by queue position (set b & 1; null queue: path id = position);
             // bounce 0: the camera origin, directions from k_generate in set 0
