@@ -950,20 +950,28 @@ __global__ __launch_bounds__(RTG_TB) void k_accumulate(ChunkArgs a, PathBufs p, 
     film[(size_t)pixel * 3 + 2] = fb;
 }
 
-// Several samples per pixel (pid = lp * ns + sl): one wave per pixel, lane = sample, so the contrib reads
-// are contiguous. Each lane folds its path's right-nested sum; then lanes 0-2 (R, G, B) add the
-// samples to the film in sample order from LDS: the same additions in the same order as
+// Several samples per pixel (pid = lp * ns + sl): lane = sample, so the contrib reads are
+// contiguous. ns >= 33: one wave per pixel, 64 samples at a time; ns <= 32: one group of
+// max(ns, 4) lanes per pixel, as many groups as fit in a wave (C5's 16-sample chunks would otherwise
+// leave 3/4 of the lanes idle). Each lane folds its path's right-nested sum; then lanes 0-2 of a pixel's group (R, G, B)
+// add its samples to the film in sample order from LDS: the same additions in the same order as
 // k_accumulate, so the same bits.
 __global__ __launch_bounds__(RTG_TB) void k_accumulate_pm(ChunkArgs a, PathBufs p, float* film) {
     __shared__ float s_acc[RTG_TB / 64][64][4];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-    const unsigned lp = blockIdx.x * (RTG_TB / 64) + wave;
-    const bool active = lp < a.npix;  // wave-uniform
+    const unsigned gw = a.ns < 4 ? 4u : a.ns;          // lanes per pixel group (>= 3: R, G, B folds)
+    const unsigned ppw = a.ns <= 32 ? 64u / gw : 1u;   // pixels per wave
+    const unsigned grp = ppw > 1 ? (unsigned)lane / gw : 0u;
+    const unsigned lp = (blockIdx.x * (RTG_TB / 64) + wave) * ppw + grp;
+    const bool active = grp < ppw && lp < a.npix;
     const unsigned pixel = active ? a.pixlist[lp] : 0u;
-    float fc = (active && lane < 3) ? film[(size_t)pixel * 3 + lane] : 0.0f;
-    for (unsigned s0 = 0; s0 < a.ns; s0 += 64) {
-        const unsigned sl = s0 + lane;
+    const unsigned first = ppw > 1 ? grp * gw : 0u;    // the group's first lane
+    const unsigned ch = (unsigned)lane - first;        // the channel this lane folds (0-2)
+    float fc = (active && ch < 3) ? film[(size_t)pixel * 3 + ch] : 0.0f;
+    const unsigned step = ppw > 1 ? a.ns : 64u;
+    for (unsigned s0 = 0; s0 < a.ns; s0 += step) {
+        const unsigned sl = s0 + ((unsigned)lane - first);
         float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (active && sl < a.ns) {
             const unsigned pid = lp * a.ns + sl;
@@ -978,12 +986,12 @@ __global__ __launch_bounds__(RTG_TB) void k_accumulate_pm(ChunkArgs a, PathBufs 
         s_acc[wave][lane][1] = acc.y;
         s_acc[wave][lane][2] = acc.z;
         __syncthreads();
-        const unsigned cnt = min(64u, a.ns - s0);
-        if (active && lane < 3)
-            for (unsigned j = 0; j < cnt; ++j) fc = fc + s_acc[wave][j][lane];
+        const unsigned cnt = min(step, a.ns - s0);
+        if (active && ch < 3)
+            for (unsigned j = 0; j < cnt; ++j) fc = fc + s_acc[wave][first + j][ch];
         __syncthreads();
     }
-    if (active && lane < 3) film[(size_t)pixel * 3 + lane] = fc;
+    if (active && ch < 3) film[(size_t)pixel * 3 + ch] = fc;
 }
 
 // sampleTileWithWeight's splat (Renderer.h:661-670): film += (sum of n samples) / (float)n for the
@@ -1928,10 +1936,12 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, st, pb.ctr, maxb, h->d_stats);
         LAUNCH_OK("k_tally");
         timed_begin(h, st, k);
-        if (a.ns > 1)
-            hipLaunchKernelGGL(k_accumulate_pm, dim3((h->npix + RTG_TB / 64 - 1) / (RTG_TB / 64)), dim3(RTG_TB), 0, st, a,
+        if (a.ns > 1) {
+            const unsigned ppw = a.ns <= 32 ? 64u / (a.ns < 4 ? 4u : a.ns) : 1u;  // pixels per wave (k_accumulate_pm)
+            const unsigned waves = (h->npix + ppw - 1) / ppw;
+            hipLaunchKernelGGL(k_accumulate_pm, dim3((waves + RTG_TB / 64 - 1) / (RTG_TB / 64)), dim3(RTG_TB), 0, st, a,
                                pb, h->d_film);
-        else
+        } else
             hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, pb, h->d_film);
         LAUNCH_OK("k_accumulate");
         timed_end(h, st, k); kinds.push_back(2); ++k;
