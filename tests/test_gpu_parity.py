@@ -170,6 +170,18 @@ def test_tiles_and_chunks_compose(cornell256):
     assert_bitexact(rt4.film()[0], full, "resume")
 
 
+@pytest.mark.parametrize("w,h,spp,max_paths", [(1, 1, 1, 0), (17, 15, 1, 0), (16, 16, 1, 0), (33, 31, 3, 0),
+                                               (64, 35, 2, 0), (33, 31, 3, 300)])
+def test_queue_segment_edges(w, h, spp, max_paths):
+    """Segmented queues (8 segments of ceil(ceil(P / 256) / 8) tiles each; k_shade's grid from the
+    read-back counts): P = 1 (seven empty segments), 255, 256, 3069 and 4480 paths, and chunks of at
+    most 300 paths, at depth 8 so later bounces empty whole segments: bit-exact vs the oracle."""
+    s = loadScene(os.path.join(SCENES, "cornell-mat"), width=w, height=h)
+    film = gpu_film(s, spp, seed=7, max_depth=8, max_paths=max_paths)
+    ref, _ = Oracle(s, 8, "rtm").render(spp, seed=7, threads=8)
+    assert_bitexact(film, ref, "%dx%d x%d spp, max_paths %d" % (w, h, spp, max_paths))
+
+
 @pytest.mark.parametrize("name", ["cornell256", "synth20k"])
 @pytest.mark.parametrize("cull", [True, False])
 def test_ray_queries_match_reference(name, cull, cornell256, synth20k):
