@@ -138,8 +138,10 @@ def parse():
                    help="comma-separated device list for the native group path (repeats rehearse ranks)")
     p.add_argument("--config", default="C3", choices=sorted(CONFIGS),
                    help="BASELINE.json config; C3 is the headline metric, the others are side measurements")
-    p.add_argument("--steps", type=int, default=3)
-    p.add_argument("--warmup", type=int, default=1)
+    # default K / W: about 10 s of timed GPU work on the headline config (the driver's utilisation
+    # sampler sees a busy GPU), one or a few frames on the long configs
+    p.add_argument("--steps", type=int, default=None)
+    p.add_argument("--warmup", type=int, default=None)
     p.add_argument("--width", type=int, default=0, help="0 = the config's")
     p.add_argument("--height", type=int, default=0, help="0 = the config's")
     p.add_argument("--spp", type=int, default=0, help="0 = the config's")
@@ -157,6 +159,10 @@ def parse():
     p.add_argument("--max-paths", type=int, default=0, help="paths per wavefront chunk (0 = library default)")
     a = p.parse_args()
     c = CONFIGS[a.config]
+    if a.steps is None:
+        a.steps = {"C2": 200, "C3": 120, "C4": 3, "C5": 1}[a.config]
+    if a.warmup is None:
+        a.warmup = {"C2": 5, "C3": 5, "C4": 1, "C5": 1}[a.config]
     a.width = a.width or c["width"]
     a.height = a.height or c["height"]
     a.spp = a.spp or c["spp"]
