@@ -291,14 +291,11 @@ def main():
     rt.set_options(flags=base)
 
     film_check = None
+    group_reduced = None
     if group_devs is not None and a.verify_film:
         rt.clear()
         rt.render(a.spp, first_sample=0)
-        reduced = rt.film()[0]
-        solo = RayTracer(scene, device=group_devs[0], max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
-        solo.render(a.spp, first_sample=0)
-        film_check = bool(np.array_equal(reduced.view(np.uint32), solo.film()[0].view(np.uint32)))
-        del solo
+        group_reduced = rt.film()[0]  # checked against one handle once the group is released
     if world > 1 and a.verify_film:
         step()  # a fresh reduced film
         barrier_sync()
@@ -323,6 +320,18 @@ def main():
                       "reduce_ms_per_step": round(float(np.mean(timed_reduce)), 3) if timed_reduce else None,
                       "rank_kernel_ms_last_step": [{"trace": round(r["extend_ms"], 2), "shade": round(r["shade_ms"], 2),
                                                     "render": round(r["render_ms"], 2)} for r in timed_ranks]}
+        group_parallelism = ("tile-sharded x%d, one process (rtg_group: a handle and host thread per device) + "
+                             "%s film reduce" % (len(group_devs), "RCCL ncclReduce" if rt.g.uses_rccl
+                                                 else "host-memory (repeated devices)"))
+        if group_reduced is not None:
+            # the group's device memory goes first (ranks rehearsed on one device hold a chunk each)
+            del rt
+            import gc
+            gc.collect()
+            solo = RayTracer(scene, device=group_devs[0], max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
+            solo.render(a.spp, first_sample=0)
+            film_check = bool(np.array_equal(group_reduced.view(np.uint32), solo.film()[0].view(np.uint32)))
+            del solo
     totals = np.array([ext_rays, shadow_rays, paths, extend_ms, extend_launches,
                        cs["node_visits"], cs["tri_tests"], cs["extension_rays"],
                        cw["node_visits"], cw["tri_tests"],
@@ -443,9 +452,7 @@ def main():
                        "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
                        "max_depth": a.max_depth,
                        "parallelism": ("tile-sharded x%d + RCCL film reduce" % world if group_devs is None else
-                                       "tile-sharded x%d, one process (rtg_group: a handle and host thread per device) + "
-                                       "%s film reduce" % (len(group_devs), "RCCL ncclReduce" if rt.g.uses_rccl
-                                                           else "host-memory (repeated devices)"))},
+                                       group_parallelism)},
             "roofline": {"bound": "dependent-random-record-fetches", "kernel": "k_trace (extension + shadow rays)",
                          "achieved": None if achieved_rec is None else round(achieved_rec, 1),
                          "peak": (round(replay["ceiling_g_fetches_per_s"], 1) if replay else
