@@ -163,7 +163,11 @@ int  rtg_set_integrator(rtg_handle* h, int integrator);
 /* Add samples [first_sample, first_sample+n_samples) of every pixel in the listed 32x32 tiles
  * (tile id = ty*tilesX + tx, RTBase TILE_SIZE=32; tile_ids=NULL = all tiles) to the film, in
  * sample order per pixel. Equivalent to n_samples calls of RayTracer::render() with the
- * deterministic sampler. Synchronous unless rtg_render_async is used.
+ * deterministic sampler. Synchronous unless rtg_render_async is used. rtg_render_async returns
+ * once its last launch is queued: the host thread reads each bounce's queue counts back while that
+ * bounce's traversal runs (the shading launch of a bounce covers only its live tiles), so it
+ * returns while the last traversal, the accumulation and the film update still run;
+ * rtg_synchronize waits for them.
  * Sample indices must stay below RTG_MAX_SAMPLES_PER_KEY: the PCG stream of (pixel, sample) is
  * keyed seq = pixel << 16 | sample; more samples take another seed. */
 #define RTG_MAX_SAMPLES_PER_KEY 65536u
