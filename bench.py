@@ -451,7 +451,8 @@ def main():
                            a.width, a.height, a.spp, a.max_depth),
                        "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
                        "max_depth": a.max_depth,
-                       "parallelism": ("tile-sharded x%d + RCCL film reduce" % world if group_devs is None else
+                       "parallelism": ("tile-sharded x%d + %s film reduce" % (world, "RCCL" if backend == "nccl" else backend)
+                                       if group_devs is None else
                                        group_parallelism)},
             "roofline": {"bound": "dependent-random-record-fetches", "kernel": "k_trace (extension + shadow rays)",
                          "achieved": None if achieved_rec is None else round(achieved_rec, 1),
