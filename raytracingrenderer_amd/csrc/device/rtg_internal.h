@@ -14,11 +14,15 @@
 using namespace rtgd;
 
 #define RTG_TB 256          // threads per block (4 waves)
+#ifndef RTG_TTB
+#define RTG_TTB 64          // threads per k_trace block: one wave, so a drained wave gives its CU slot
+                            // back at once (256: C3 -0.4 %, shard-of 8 -0.6 %, profiles/r03_trace_block_ab.txt)
+#endif
 #define RTG_POP ((int)0x80000001)  // "pop the stack" marker inside one traversal step
 // Measured constants of the traversal and shading kernels (DESIGN.md §4 records the A/B runs;
 // the rejected alternatives are archived under tools/experiments/, not compiled in):
 #ifndef RTG_STACK
-#define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (24 KB per block)
+#define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (96 B per lane)
 #endif
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)

@@ -57,10 +57,10 @@ static __device__ __forceinline__ void trace_slice(const TraceIO& io, unsigned n
 }
 
 template <bool COUNT>
-__global__ __launch_bounds__(RTG_TB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
+__global__ __launch_bounds__(RTG_TTB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
 void k_trace(SceneView s, TraceIO io) {
-    __shared__ int stk[RTG_STACK][RTG_TB];
-    __shared__ float kstk[COUNT ? RTG_STACK : 1][RTG_TB];  // COUNT only: entry key of each push
+    __shared__ int stk[RTG_STACK][RTG_TTB];
+    __shared__ float kstk[COUNT ? RTG_STACK : 1][RTG_TTB];  // COUNT only: entry key of each push
     const int tid = threadIdx.x;
     const int lane = lane_id();
     const unsigned gthreads = gridDim.x * blockDim.x;
@@ -1106,7 +1106,7 @@ int ensure_ovf(rtg_handle* h) {
     // at least one BVH2 level)
     size_t deep = std::max<size_t>(h->bvh_depth, (size_t)h->wide_depth * 3) + 2;
     size_t levels = deep > RTG_STACK ? deep - RTG_STACK : 1;
-    size_t need = levels * (size_t)grid * RTG_TB;
+    size_t need = levels * (size_t)grid * RTG_TTB;
     if (need <= h->cap_ovf) return RTG_OK;
     (void)hipFree(h->d_ovf);
     HIPOK(hipMalloc((void**)&h->d_ovf, need * sizeof(int)));
@@ -1637,10 +1637,10 @@ int upload_scene(int device, const HostScene& hs, rtg_handle* h) {
     for (auto& e : h->ev) HIPOK(hipEventCreate(&e));
 
     int occ = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false>, RTG_TB, 0));
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false>, RTG_TTB, 0));
     h->trace_blocks = h->n_cu * std::max(1, occ);
     int occ3 = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_trace<true>, RTG_TB, 0));
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_trace<true>, RTG_TTB, 0));
     h->trace_blocks_count = h->n_cu * std::max(1, occ3);
     return ensure_ovf(h);
 }
@@ -1747,8 +1747,8 @@ int launch_generate(rtg_handle* h, const ChunkArgs& a, const PathBufs& pb, hipSt
 }
 
 int launch_trace(rtg_handle* h, const TraceIO& io, hipStream_t st) {
-    if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
-    else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
+    if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TTB), 0, st, h->sv, io);
+    else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, st, h->sv, io);
     LAUNCH_OK("k_trace");
     return RTG_OK;
 }
@@ -1811,7 +1811,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     io.ovf = h->d_ovf;
     // RTG_DEBUG builds with RTG_OPT_WAVETIME: per-wave clocks of chunk 0's trace launches, on stderr
     unsigned long long* d_wt = nullptr;
-    const size_t wt_waves = (size_t)std::max(h->trace_blocks, h->trace_blocks_count) * (RTG_TB / 64);
+    const size_t wt_waves = (size_t)std::max(h->trace_blocks, h->trace_blocks_count) * (RTG_TTB / 64);
     if (RTG_DEBUG && h->wavetime) {
         HIPOK(hipMalloc((void**)&d_wt, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long)));
         HIPOK(hipMemsetAsync(d_wt, 0, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long), st));
@@ -1928,8 +1928,8 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                 io.cap_n = (unsigned)cn;
             }
             timed_begin(h, st, k);
-            if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TB), 0, st, h->sv, io);
-            else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, st, h->sv, io);
+            if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TTB), 0, st, h->sv, io);
+            else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, st, h->sv, io);
             LAUNCH_OK("k_trace");
             timed_end(h, st, k); kinds.push_back(0); ++k;
         }
@@ -2144,7 +2144,7 @@ int rtg_debug_replay(rtg_handle* h, double* out) {
         HIPOK(hipMemsetAsync(d_f8, 0, 8 * 32 * sizeof(unsigned), h->stream));
         HIPOK(hipMemsetAsync(d_tot, 0, sizeof(unsigned long long), h->stream));
         HIPOK(hipEventRecord(e0, h->stream));
-        hipLaunchKernelGGL(k_replay, dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, (const uint4*)h->d_cap,
+        hipLaunchKernelGGL(k_replay, dim3(std::max(1, h->trace_blocks * RTG_TTB / RTG_TB)), dim3(RTG_TB), 0, h->stream, h->sv, (const uint4*)h->d_cap,
                            (const unsigned*)h->d_cap_len, (const unsigned*)h->d_cap_rays, h->cap_n, 0u, d_f8, d_tot,
                            d_out);
         LAUNCH_OK("k_replay");
@@ -2287,7 +2287,7 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
         io.count = h->d_qctr;
         io.hits = (float4*)d_out;
     }
-    hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TB), 0, h->stream, h->sv, io);
+    hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, h->stream, h->sv, io);
     HIPOK(hipGetLastError());
     HIPOK(hipStreamSynchronize(h->stream));
     if (any) HIPOK(hipMemcpy(vis, d_out, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
