@@ -24,17 +24,28 @@ using namespace rtgd;
 #ifndef RTG_STACK
 #define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (96 B per lane)
 #endif
+// (the tuning constants are overridable with -D for A/B builds: tools/ab_matrix.sh)
+#ifndef RTG_POSTPONE
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
+#endif
+#ifndef RTG_REFILL
 #define RTG_REFILL 12       // refill idle lanes once at least this many are idle (the setup code then
                             // runs with more lanes per execution)
+#endif
 #ifndef RTG_TRACE_WPE
 #define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel (80 VGPRs)
 #endif
 #define RTG_CULL_REL 1.52587890625e-05f  // 2^-16 relative inflation for distance culling
+#ifndef RTG_FETCH
 #define RTG_FETCH 256       // rays a wave takes from a work counter per atomic (k_trace pool)
+#endif
+#ifndef RTG_FETCH_TAIL
 #define RTG_FETCH_TAIL 8    // fetch RTG_TAIL_BATCH rays per atomic once about this many rounds of
-#define RTG_TAIL_BATCH 64   // big batches are left in the slice (shorter drain tails)
+#endif                      // big batches are left in the slice (shorter drain tails)
+#ifndef RTG_TAIL_BATCH
+#define RTG_TAIL_BATCH 64
+#endif
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 7   // min waves per SIMD for k_shade (72 VGPRs, no spills; one tile per block)
 #endif
