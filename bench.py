@@ -157,12 +157,18 @@ def parse():
     p.add_argument("--verify-film", action="store_true",
                    help="N>1: every tile re-rendered on one device, compared with the reduced film bit for bit")
     p.add_argument("--max-paths", type=int, default=0, help="paths per wavefront chunk (0 = library default)")
+    p.add_argument("--dropin-frames", type=int, default=None,
+                   help="frames of the drop-in leg (one 1-spp render call per frame, Main.cpp's loop); 0 = skip; "
+                        "default 64 on C2 / C3, 0 otherwise")
+    p.add_argument("--dropin-reps", type=int, default=3)
     a = p.parse_args()
     c = CONFIGS[a.config]
     if a.steps is None:
         a.steps = {"C2": 200, "C3": 120, "C4": 3, "C5": 1}[a.config]
     if a.warmup is None:
         a.warmup = {"C2": 5, "C3": 5, "C4": 1, "C5": 1}[a.config]
+    if a.dropin_frames is None:
+        a.dropin_frames = 64 if a.config in ("C2", "C3") and a.shard_of <= 1 else 0
     a.width = a.width or c["width"]
     a.height = a.height or c["height"]
     a.spp = a.spp or c["spp"]
@@ -279,6 +285,11 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t_start
 
+    # the drop-in frame loop (Main.cpp:74-118): one RayTracer::render() = one rtg call of 1 spp
+    dropin = None
+    if world == 1 and group_devs is None and a.dropin_frames > 0:
+        dropin = dropin_leg(rt, a, tiles)
+
     # counting passes (untimed): box / triangle tests per closest-hit ray on the same workload.
     # Algorithmic work is the reference's BVH2 walk; the 4-wide walk's own tests are reported too.
     def count(flags):
@@ -350,6 +361,9 @@ def main():
     rays = ext_rays + shadow_rays
     mrays = rays / t_max / 1e6
     ms_step = t_max * 1e3 / a.steps
+    if dropin is not None:
+        dropin["batched_ms_per_frame"] = round(ms_step / a.spp, 4)
+        dropin["queued_over_batched"] = round(dropin["queued"]["ms_per_frame"] / (ms_step / a.spp), 3)
 
     # roofline for the dominant kernel, k_trace (one launch per bounce traces the extension rays of
     # bounce b and the shadow rays of bounce b-1). Its limiter is the memory system's throughput of
@@ -541,6 +555,7 @@ def main():
             "kernel_ms_per_step_rank0": {"trace": round(local_kernel_ms[0] / a.steps, 2),
                                          "generate_shade_accumulate": round(local_kernel_ms[2] / a.steps, 2)},
             "cpu_baseline": cpu,
+            **({"dropin": dropin} if dropin is not None else {}),
             **({"film_reduce_bit_exact": film_check} if film_check is not None else {}),
             **({"group": group_info} if group_info is not None else {}),
             "setup_s": round(setup_s, 2),
@@ -548,6 +563,48 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dropin_leg(rt, a, tiles):
+    """C3 through the drop-in frame loop: RTBase's Main.cpp calls RayTracer::render() once per frame
+    (Main.cpp:74-118), and render() adds one sample per pixel (Renderer.h:876-885). Each frame here
+    is one 1-spp librtg call, a.dropin_frames frames per repetition, under three host policies:
+      queued      rtg_render_async(1 spp) per frame (what integration/rtg_rtbase.h's rtg_render_frame
+                  does), the film read back once at the end (saveHDR): frames overlap on the GPU
+      sync        rtg_render(1 spp) per frame (returns when the frame is on the film), one read at the end
+      sync_read   rtg_render + rtg_film_read (12.6 MB D2H) every frame: round 3's rtg_render_frame
+    The film of every policy is compared bit for bit with one batched render of the same samples."""
+    F = a.dropin_frames
+    out = {"frames_per_rep": F, "reps": a.dropin_reps, "spp_per_call": 1,
+           "reference": "Main.cpp:74-118 frame loop, RayTracer::render() = 1 spp (Renderer.h:876-885)"}
+    rt.clear()
+    rt.render(F, tiles=tiles, first_sample=0)
+    batch_film = rt.film()[0].view(np.uint32).copy()
+
+    def run(policy):
+        best = None
+        same = True
+        rays = 0
+        for _ in range(a.dropin_reps):
+            rt.clear()
+            rt.synchronize()
+            t0 = time.perf_counter()
+            for f in range(F):
+                rt.render(1, tiles=tiles, first_sample=f, sync=(policy != "queued"))
+                if policy == "sync_read":
+                    rt.film()
+            film = rt.film()[0]
+            dt = time.perf_counter() - t0
+            st = rt.stats()
+            rays = st["extension_rays"] + st["shadow_rays"]
+            same = same and bool(np.array_equal(film.view(np.uint32), batch_film))
+            best = dt if best is None or dt < best else best
+        return {"ms_per_frame": round(best * 1e3 / F, 4), "mrays_per_s": round(rays / best / 1e6, 1),
+                "film_equals_batched": same}
+    for pol in ("queued", "sync", "sync_read"):
+        out[pol] = run(pol)
+    out["batched_ms_per_frame"] = None  # filled by the caller (ms_per_step / spp of the headline)
+    return out
 
 
 def host_cores():

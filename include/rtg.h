@@ -31,8 +31,9 @@
 extern "C" {
 #endif
 
-/* 2: rtg_scene_desc.projection; 3: rtg_stats.tri_tail_loads / leafbox_tests appended */
-#define RTG_ABI_VERSION 3
+/* 2: rtg_scene_desc.projection; 3: rtg_stats.tri_tail_loads / leafbox_tests appended;
+ * 4: rtg_render_async queues frames (returns before any of its work has run), rtg_render_idle */
+#define RTG_ABI_VERSION 4
 
 /* error codes */
 #define RTG_OK              0
@@ -135,7 +136,8 @@ void rtg_destroy(rtg_handle* h);
  * most max_depth+2 closest-hit segments. flags: RTG_OPT_CULL enables the conservative distance
  * culling (without it traversal visits exactly the reference's node set: verification mode);
  * RTG_OPT_COUNT runs the counting kernels (node / triangle tests in rtg_stats);
- * RTG_OPT_TIMING records HIP events around every launch (per-kernel-class ms in rtg_stats);
+ * RTG_OPT_TIMING records HIP events around every launch (per-kernel-class ms in rtg_stats; implies
+ * RTG_OPT_SERIAL);
  * RTG_OPT_BVH2 forces the reference BVH2 walk (no 4-wide collapse; verification / A-B).
  * max_paths_in_flight bounds the paths of one wavefront chunk (0 = keep, default 1G; a chunk's path
  * state is also held to half the free HBM). */
@@ -144,6 +146,8 @@ void rtg_destroy(rtg_handle* h);
 #define RTG_OPT_TIMING 4
 #define RTG_OPT_BVH2   8
 #define RTG_OPT_WAVETIME 16  /* diagnostic builds only (RTG_DEBUG=1): per-wave clocks of k_trace on stderr */
+#define RTG_OPT_SERIAL  32   /* one chunk in flight at a time, every k_shade grid sized from the live counts
+                                read back during the traversal (verification / A-B of the frame pipeline) */
 int  rtg_set_options(rtg_handle* h, int max_depth, int flags, uint32_t max_paths_in_flight);
 
 /* Per-pixel estimator (the alternative RayTracer methods of Renderer.h). PATH is RayTracer::render's
@@ -163,11 +167,20 @@ int  rtg_set_integrator(rtg_handle* h, int integrator);
 /* Add samples [first_sample, first_sample+n_samples) of every pixel in the listed 32x32 tiles
  * (tile id = ty*tilesX + tx, RTBase TILE_SIZE=32; tile_ids=NULL = all tiles) to the film, in
  * sample order per pixel. Equivalent to n_samples calls of RayTracer::render() with the
- * deterministic sampler. Synchronous unless rtg_render_async is used. rtg_render_async returns
- * once its last launch is queued: the host thread reads each bounce's queue counts back while that
- * bounce's traversal runs (the shading launch of a bounce covers only its live tiles), so it
- * returns while the last traversal, the accumulation and the film update still run;
- * rtg_synchronize waits for them.
+ * deterministic sampler.
+ * rtg_render returns when the samples are on the film. rtg_render_async only queues them:
+ *   - with hip_stream NULL it is the drop-in RayTracer::render() of a frame loop (Main.cpp:74-118).
+ *     A call of at most 8M paths (n_samples x pixels; a 1-spp frame up to 8 Mpixel) is queued
+ *     without any host wait and returns before its work starts; consecutive calls run side by side
+ *     on the GPU (up to 3 frames in flight, each with its own path state), their film updates still
+ *     in sample order, so the film is bit-identical to one rtg_render of all the samples. Larger calls
+ *     read each bounce's live count back during the traversal and return once their last launch is
+ *     queued. Anything that reads the film or the stats (rtg_film_read with a film pointer,
+ *     rtg_film_copy_device, rtg_get_stats, rtg_synchronize, rtg_clear ...) first waits for the
+ *     queued frames; rtg_film_read(h, NULL, &spp) returns Film::SPP at once.
+ *   - with a hip_stream, the work is ordered after the caller's earlier work on that stream, and
+ *     the caller's later work on it sees the film updated.
+ * rtg_render_idle sets *idle to 1 when no queued render work is left on the GPU.
  * Sample indices must stay below RTG_MAX_SAMPLES_PER_KEY: the PCG stream of (pixel, sample) is
  * keyed seq = pixel << 16 | sample; more samples take another seed. */
 #define RTG_MAX_SAMPLES_PER_KEY 65536u
@@ -176,6 +189,7 @@ int  rtg_render(rtg_handle* h, uint32_t first_sample, uint32_t n_samples, uint64
 int  rtg_render_async(rtg_handle* h, uint32_t first_sample, uint32_t n_samples, uint64_t seed,
                       const uint32_t* tile_ids, uint32_t n_tiles, void* hip_stream);
 int  rtg_synchronize(rtg_handle* h);
+int  rtg_render_idle(rtg_handle* h, int* idle);
 
 /* RayTracer::adaptiveRender (Renderer.h:583-749), one frame (Film::SPP += 1). Pass 1 renders
  * init_samples samples of every pixel (sample indices first_sample ...) into a scratch film and

@@ -8,6 +8,11 @@
  *                                             glibc's own sinf/cosf) and acosf on every float
  *                                             bit pattern in [first, last] (default: all 2^32),
  *                                             or every stride-th one
+ *   libm_check digest [stride]                 no C library call: FNV-1a digests of rtg_math.h's own
+ *                                             outputs on every stride-th float (default 31) and
+ *                                             2^20 splitmix64 atan2f pairs, plus the host's glibc
+ *                                             version and FMA/AVX2 flags (tests/golden/rtm_digest.json
+ *                                             pins the digests where glibc 2.35's FMA build matched)
  *   libm_check atan2 [log2_pairs]              atan2f on 2^k pairs (default 2^30): random bit
  *                                             patterns, unit-vector components (the reference's
  *                                             EnvironmentMap::evaluate inputs, Lights.h:152),
@@ -25,6 +30,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <gnu/libc-version.h>
 
 #include "../include/rtg_math.h"
 
@@ -141,9 +147,45 @@ static void* work(void* arg)
     return NULL;
 }
 
+static uint64_t fnv(uint64_t h, float v)
+{
+    uint32_t b = v != v ? 0x7fc00000u : rtm_asuint(v);  /* any NaN hashes as the canonical one */
+    for (int k = 0; k < 4; ++k) { h ^= (b >> (8 * k)) & 0xffu; h *= 0x100000001b3ull; }
+    return h;
+}
+
+static int digest_mode(uint64_t stride)
+{
+    uint64_t hs = 0xcbf29ce484222325ull, hc = hs, hsc = hs, ha = hs, ht = hs;
+    for (uint64_t i = 0; i < (1ull << 32); i += stride) {
+        const float x = rtm_asfloat((uint32_t)i);
+        float s, c;
+        rtm_sincosf(x, &s, &c);
+        hs = fnv(hs, rtm_sinf(x));
+        hc = fnv(hc, rtm_cosf(x));
+        hsc = fnv(fnv(hsc, s), c);
+        ha = fnv(ha, rtm_acosf(x));
+    }
+    uint64_t z = 0x9e3779b97f4a7c15ull;
+    for (int i = 0; i < (1 << 20); ++i) {
+        uint64_t r = (z += 0x9e3779b97f4a7c15ull);
+        r = (r ^ (r >> 30)) * 0xbf58476d1ce4e5b9ull;
+        r = (r ^ (r >> 27)) * 0x94d049bb133111ebull;
+        r ^= r >> 31;
+        ht = fnv(ht, rtm_atan2f(rtm_asfloat((uint32_t)r), rtm_asfloat((uint32_t)(r >> 32))));
+    }
+    printf("glibc %s fma %d avx2 %d\n", gnu_get_libc_version(), __builtin_cpu_supports("fma") ? 1 : 0,
+           __builtin_cpu_supports("avx2") ? 1 : 0);
+    printf("stride %llu sinf %016llx cosf %016llx sincosf %016llx acosf %016llx atan2f %016llx\n",
+           (unsigned long long)stride, (unsigned long long)hs, (unsigned long long)hc, (unsigned long long)hsc,
+           (unsigned long long)ha, (unsigned long long)ht);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
-    if (argc < 2) { fprintf(stderr, "usage: %s unary [first last] | atan2 [log2_pairs]\n", argv[0]); return 2; }
+    if (argc < 2) { fprintf(stderr, "usage: %s unary [first last] | atan2 [log2_pairs] | digest [stride]\n", argv[0]); return 2; }
+    if (strcmp(argv[1], "digest") == 0) return digest_mode(argc >= 3 ? strtoull(argv[2], 0, 0) : 31);
     const int mode = strcmp(argv[1], "atan2") == 0;
     uint64_t lo = 0, hi = 1ull << 32;
     uint64_t stride = 1;

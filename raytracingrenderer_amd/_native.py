@@ -10,7 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
 
 RTG_MAT_DIFFUSE, RTG_MAT_LAMBERT, RTG_MAT_MIRROR, RTG_MAT_GLASS = 0, 1, 2, 3
-RTG_OPT_CULL, RTG_OPT_COUNT, RTG_OPT_TIMING, RTG_OPT_BVH2, RTG_OPT_WAVETIME = 1, 2, 4, 8, 16
+RTG_OPT_CULL, RTG_OPT_COUNT, RTG_OPT_TIMING, RTG_OPT_BVH2, RTG_OPT_WAVETIME, RTG_OPT_SERIAL = 1, 2, 4, 8, 16, 32
 RTG_INTEGRATOR_PATH, RTG_INTEGRATOR_DIRECT, RTG_INTEGRATOR_ALBEDO, RTG_INTEGRATOR_NORMALS = 0, 1, 2, 3
 RTG_INTEGRATOR_DIRECT_MIS = 4
 
@@ -82,6 +82,7 @@ RTG_EXPORTS = [
     ("rtg_render", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32]),
     ("rtg_render_async", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, u32p, C.c_uint32, C.c_void_p]),
     ("rtg_synchronize", C.c_int, [C.c_void_p]),
+    ("rtg_render_idle", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     ("rtg_render_light", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64]),
     ("rtg_render_instant_radiosity", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32]),
     ("rtg_render_adaptive", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, u32p]),

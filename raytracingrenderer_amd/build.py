@@ -115,14 +115,14 @@ def build_ref(force=False):
 
 def stage_assets():
     """Copy reference scene data (not code) used by tests/bench into assets/ (git-ignored, travels
-    to the GPU box): coffee (config C5), bathroom (C4) and GI.hdr. Only when /root/reference is
-    present."""
+    to the GPU box): coffee (config C5), bathroom (C4), materialball (the env-lit scene) and GI.hdr.
+    Only when /root/reference is present."""
     src = "/root/reference/RTBase"
     dst = os.path.join(ROOT, "assets")
     if not os.path.isdir(src):
         return
     os.makedirs(dst, exist_ok=True)
-    for name in ("coffee", "bathroom"):
+    for name in ("coffee", "bathroom", "materialball"):
         if os.path.isdir(os.path.join(src, name)) and not os.path.isdir(os.path.join(dst, name)):
             shutil.copytree(os.path.join(src, name), os.path.join(dst, name))
     for f, into in (("GI.hdr", ""), ("GI.hdr", "coffee")):  # C5 = coffee_f + "envmap": "GI.hdr"

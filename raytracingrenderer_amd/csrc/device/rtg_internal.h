@@ -147,7 +147,8 @@ struct PathBufs {
     float4* sh_o;              // [P] NEE shadow ray origin + maxT (path tracer: at its shadow-queue position)
     float4* sh_d;              // [P] NEE shadow ray direction (same)
     float4* sh_c;              // [P] by path id: NEE value thr * Ld if visible
-    unsigned* q[2];            // extension queues of path ids (ping-pong)
+    unsigned* q[2];            // extension queues of path ids (ping-pong; light tracer and instant
+                               // radiosity only, allocated on their request: ensure_chunk(queues))
     unsigned* shq;             // shadow queue of path ids
     Counters* ctr;             // [maxb + 1]
 };
@@ -190,12 +191,39 @@ static int dev_upload(T** dst, const std::vector<T>& src) {
     return RTG_OK;
 }
 
+// Chunks in flight (the frame pipeline). A chunk of at most RTG_PIPE_MAX_P paths -- one 1-spp frame
+// of a film up to 8 Mpixel, the drop-in RayTracer::render() -- is issued without any host wait (its
+// k_shade grids cover every tile a segment can hold; blocks past the live count exit at once) into the
+// next of RTG_SLOTS slots, each with its own path state, stack overflow and stream, so consecutive
+// frames run side by side on the GPU and fill each other's drain tails. The film folds stay in sample
+// order: a chunk's k_accumulate waits for the previous chunk's (rtg_handle::last_fold). Larger chunks
+// run in slot 0 alone and size each k_shade grid from the live counts read back during the
+// traversal (a grid of every possible tile costs more than the wait there).
+#ifndef RTG_SLOTS
+#define RTG_SLOTS 3                        // with the handle's stream, 4 = GPU_MAX_HW_QUEUES streams
+#endif
+#ifndef RTG_PIPE_MAX_P
+#define RTG_PIPE_MAX_P (8u << 20)
+#endif
+#ifndef RTG_HOSTGRID_MIN_TILES
+#define RTG_HOSTGRID_MIN_TILES 4096u       // big chunks: seg_tiles at or above this size the k_shade grid
+#endif                                     // from the read-back counts
+struct ChunkSlot {
+    PathBufs pb{};
+    size_t cap_P = 0;           // paths the buffers hold
+    int cap_maxb = 0;           // contribution planes they hold
+    int* d_ovf = nullptr;       // k_trace's stack overflow [level][thread] for launches of this slot
+    size_t cap_ovf = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t fold = nullptr;  // this slot's last film fold (k_accumulate) has run
+};
+
 struct rtg_handle {
     int device = 0;
     hipStream_t stream = nullptr;
     int W = 0, H = 0;
     uint32_t spp = 0;
-    int max_depth = 4, cull = 1, count = 0, timing = 0;
+    int max_depth = 4, cull = 1, count = 0, timing = 0, serial = 0;
     uint32_t max_paths = 1u << 30;  // 1G paths in flight at most; the chunk is held to half the free HBM
     int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0;
     int wavetime = 0;  // RTG_DEBUG builds: per-wave clocks of the first chunk (RTG_OPT_WAVETIME)
@@ -223,16 +251,17 @@ struct rtg_handle {
     DevTex* d_texinfo = nullptr;
     float* d_texels = nullptr;
     float* d_film = nullptr;
-    // chunk buffers (path state of the paths in flight)
-    size_t cap_P = 0;
-    int cap_maxb = 0;
-    PathBufs pb{};
+    // chunk buffers (path state of the paths in flight), one set per slot; slot 0 also serves the
+    // light tracer, instant radiosity and the ray queries (on `stream`)
+    ChunkSlot slot[RTG_SLOTS];
+    unsigned next_slot = 0;        // the pipeline's next slot
+    hipEvent_t entry = nullptr;    // recorded on the caller's stream when a render starts: chunks wait on it
+    hipEvent_t last_fold = nullptr;  // the last queued chunk's fold (a slot's event; null before any)
+    bool inflight = false;         // chunks queued by rtg_render_async(.., NULL) not yet joined to `stream`
     unsigned* d_pix = nullptr;
     size_t cap_pix = 0;
     std::vector<uint32_t> pix_key;
     unsigned npix = 0;
-    int* d_ovf = nullptr;
-    size_t cap_ovf = 0;
     unsigned* d_qctr = nullptr;  // query-API counters [4]
     unsigned long long* d_stats = nullptr;
     rtg_stats stats{};
@@ -274,11 +303,17 @@ struct HostScene {
 // rtg_kernels.hip
 int prepare_scene(const rtg_scene_desc* d, HostScene& hs);
 int upload_scene(int device, const HostScene& hs, rtg_handle* h);
-int ensure_ovf(rtg_handle* h);
+int ensure_ovf(rtg_handle* h, ChunkSlot& sl);
 int set_pixels(rtg_handle* h, const uint32_t* tiles, uint32_t n_tiles);
-int ensure_chunk(rtg_handle* h, size_t P, int maxb);
+// path state of P paths with maxb contribution planes in slot sl (+ the id queues q[0..1] if asked)
+int ensure_chunk(rtg_handle* h, ChunkSlot& sl, size_t P, int maxb, bool queues);
+// lazy: chunks stay queued past the return (rtg_render_async with no stream); join_frames later makes
+// the handle's stream wait for them. Otherwise `st` waits for them before render_impl returns.
 int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed, const uint32_t* tiles,
-                uint32_t n_tiles, hipStream_t st);
+                uint32_t n_tiles, hipStream_t st, bool lazy);
+// the handle's stream waits for every queued chunk (called by every entry point that reads the film,
+// the stats or slot 0's buffers, or synchronises)
+int join_frames(rtg_handle* h);
 // k_generate for the paths of a (camera rays at pixel centres, Scene.h:43-54)
 int launch_generate(rtg_handle* h, const ChunkArgs& a, const PathBufs& pb, hipStream_t st);
 // one k_trace launch (closest-hit rays of io.queue and any-hit rays of io.squeue) on stream st

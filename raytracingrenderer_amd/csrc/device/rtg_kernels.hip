@@ -1060,29 +1060,53 @@ __global__ void k_tally(const Counters* ctr, int maxb, unsigned long long* stats
 
 // ================================================================== host side (C-ABI)
 thread_local std::string g_err;
-static void free_chunk(rtg_handle* h) {
-    PathBufs& p = h->pb;
+static void free_chunk(ChunkSlot& sl) {
+    PathBufs& p = sl.pb;
+    if (sl.stream) (void)hipStreamSynchronize(sl.stream);  // queued launches may still use the buffers
     (void)hipFree(p.thr); (void)hipFree(p.rng); (void)hipFree(p.meta); (void)hipFree(p.contrib);
     (void)hipFree(p.q[0]); (void)hipFree(p.q[1]); (void)hipFree(p.hits); (void)hipFree(p.shq); (void)hipFree(p.ctr);
     (void)hipFree(p.ray_o); (void)hipFree(p.ray_d);
     (void)hipFree(p.thr2); (void)hipFree(p.rng2); (void)hipFree(p.ray_o2); (void)hipFree(p.ray_d2);
     (void)hipFree(p.sh_o); (void)hipFree(p.sh_d); (void)hipFree(p.sh_c);
     p = PathBufs{};
-    h->cap_P = 0;
-    h->cap_maxb = 0;
+    sl.cap_P = 0;
+    sl.cap_maxb = 0;
 }
 
-int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
-    if (P <= h->cap_P && maxb <= h->cap_maxb) return RTG_OK;
-    free_chunk(h);
-    PathBufs& p = h->pb;
+// bytes of path state per path: 200 B of payload and queue arrays, 16 B per contribution plane, and
+// 8 B for the id queues (light tracer / instant radiosity only)
+static size_t path_bytes(int planes, bool queues) { return (size_t)200 + (size_t)16 * (size_t)planes + (queues ? 8u : 0u); }
+static size_t slot_bytes(const ChunkSlot& sl) { return sl.cap_P * path_bytes(sl.cap_maxb, sl.pb.q[0] != nullptr); }
+
+static int ensure_stream(ChunkSlot& sl) {
+    if (!sl.stream) HIPOK(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+    if (!sl.fold) HIPOK(hipEventCreateWithFlags(&sl.fold, hipEventDisableTiming));
+    return RTG_OK;
+}
+
+int ensure_chunk(rtg_handle* h, ChunkSlot& sl, size_t P, int maxb, bool queues) {
+    (void)h;
+    int rc;
+    if ((rc = ensure_stream(sl))) return rc;
+    PathBufs& p = sl.pb;
+    if (P <= sl.cap_P && maxb <= sl.cap_maxb) {
+        if (queues && !p.q[0]) {
+            if (sl.stream) HIPOK(hipStreamSynchronize(sl.stream));
+            HIPOK(hipMalloc((void**)&p.q[0], sl.cap_P * sizeof(unsigned)));
+            HIPOK(hipMalloc((void**)&p.q[1], sl.cap_P * sizeof(unsigned)));
+        }
+        return RTG_OK;
+    }
+    free_chunk(sl);
     const size_t Q = queue_slots(P);  // arrays indexed by queue position (segmented queues)
     HIPOK(hipMalloc((void**)&p.thr, Q * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.rng, Q * sizeof(unsigned long long)));
     HIPOK(hipMalloc((void**)&p.meta, P * sizeof(int)));
     HIPOK(hipMalloc((void**)&p.contrib, P * (size_t)maxb * sizeof(float4)));
-    HIPOK(hipMalloc((void**)&p.q[0], P * sizeof(unsigned)));
-    HIPOK(hipMalloc((void**)&p.q[1], P * sizeof(unsigned)));
+    if (queues) {
+        HIPOK(hipMalloc((void**)&p.q[0], P * sizeof(unsigned)));
+        HIPOK(hipMalloc((void**)&p.q[1], P * sizeof(unsigned)));
+    }
     HIPOK(hipMalloc((void**)&p.shq, Q * sizeof(unsigned)));
     HIPOK(hipMalloc((void**)&p.hits, Q * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.ray_o, Q * sizeof(float4)));
@@ -1095,22 +1119,32 @@ int ensure_chunk(rtg_handle* h, size_t P, int maxb) {
     HIPOK(hipMalloc((void**)&p.sh_d, Q * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.sh_c, P * sizeof(float4)));
     HIPOK(hipMalloc((void**)&p.ctr, (size_t)(maxb + 1) * sizeof(Counters)));
-    h->cap_P = P;
-    h->cap_maxb = maxb;
+    sl.cap_P = P;
+    sl.cap_maxb = maxb;
     return RTG_OK;
 }
 
-int ensure_ovf(rtg_handle* h) {
+int ensure_ovf(rtg_handle* h, ChunkSlot& sl) {
     int grid = std::max(h->trace_blocks, h->trace_blocks_count);
     // deepest stack: one entry per BVH2 level, or up to 3 per wide level (each wide level descends
     // at least one BVH2 level)
     size_t deep = std::max<size_t>(h->bvh_depth, (size_t)h->wide_depth * 3) + 2;
     size_t levels = deep > RTG_STACK ? deep - RTG_STACK : 1;
     size_t need = levels * (size_t)grid * RTG_TTB;
-    if (need <= h->cap_ovf) return RTG_OK;
-    (void)hipFree(h->d_ovf);
-    HIPOK(hipMalloc((void**)&h->d_ovf, need * sizeof(int)));
-    h->cap_ovf = need;
+    if (need <= sl.cap_ovf) return RTG_OK;
+    if (sl.stream) HIPOK(hipStreamSynchronize(sl.stream));
+    (void)hipFree(sl.d_ovf);
+    sl.d_ovf = nullptr;
+    HIPOK(hipMalloc((void**)&sl.d_ovf, need * sizeof(int)));
+    sl.cap_ovf = need;
+    return RTG_OK;
+}
+
+int join_frames(rtg_handle* h) {
+    if (!h->inflight) return RTG_OK;
+    h->inflight = false;
+    HIPOK(hipStreamWaitEvent(h->stream, h->last_fold, 0));
+    HIPOK(hipEventRecord(h->ev[1], h->stream));  // the end of the queued run (rtg_stats::render_ms)
     return RTG_OK;
 }
 
@@ -1642,7 +1676,8 @@ int upload_scene(int device, const HostScene& hs, rtg_handle* h) {
     int occ3 = 0;
     HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_trace<true>, RTG_TTB, 0));
     h->trace_blocks_count = h->n_cu * std::max(1, occ3);
-    return ensure_ovf(h);
+    HIPOK(hipEventCreateWithFlags(&h->entry, hipEventDisableTiming));
+    return ensure_ovf(h, h->slot[0]);
 }
 
 extern "C" {
@@ -1664,11 +1699,20 @@ int rtg_create(int device, const rtg_scene_desc* desc, rtg_handle** out) {
 void rtg_destroy(rtg_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
-    free_chunk(h);
+    if (h->stream) {
+        (void)join_frames(h);
+        (void)hipStreamSynchronize(h->stream);
+    }
+    for (ChunkSlot& sl : h->slot) {
+        free_chunk(sl);
+        (void)hipFree(sl.d_ovf);
+        if (sl.fold) (void)hipEventDestroy(sl.fold);
+        if (sl.stream) (void)hipStreamDestroy(sl.stream);
+    }
+    if (h->entry) (void)hipEventDestroy(h->entry);
     (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodesq); (void)hipFree(h->d_leafbox); (void)hipFree(h->d_tris48); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
     (void)hipFree(h->d_lights); (void)hipFree(h->d_texinfo); (void)hipFree(h->d_texels); (void)hipFree(h->d_film);
-    (void)hipFree(h->d_pix); (void)hipFree(h->d_ovf); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
+    (void)hipFree(h->d_pix); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
     for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : h->kev) (void)hipEventDestroy(e);
     for (auto& e : h->cev) (void)hipEventDestroy(e);
@@ -1697,6 +1741,7 @@ int rtg_set_options(rtg_handle* h, int max_depth, int cull, uint32_t max_paths) 
     h->timing = (cull >> 2) & 1;  // bit 2: per-launch timing events
     h->wide = ((cull >> 3) & 1) ? 0 : 1;  // bit 3: force the reference BVH2 walk
     h->wavetime = RTG_DEBUG ? (cull >> 4) & 1 : 0;  // bit 4 (RTG_DEBUG builds): per-wave clocks
+    h->serial = (cull >> 5) & 1;  // bit 5: no frame pipeline, read-back k_shade grids
     if (max_paths) h->max_paths = max_paths;
     return RTG_OK;
 }
@@ -1762,8 +1807,35 @@ static void timed_end(rtg_handle* h, hipStream_t st, size_t k) {
     if (h->timing) (void)hipEventRecord(h->kev[2 * k + 1], st);
 }
 
+// RTG_DEBUG builds, RTG_OPT_WAVETIME: per launch, when the waves started, found the queue empty and ended
+static void print_wavetime(const std::vector<unsigned long long>& wt, int maxb, size_t wt_waves) {
+    for (int b = 0; b <= maxb; ++b) {
+        const unsigned long long* w = wt.data() + (size_t)b * wt_waves * 3;
+        unsigned long long t0 = ~0ull, e0 = ~0ull;
+        std::vector<double> ends, starts;
+        for (size_t i = 0; i < wt_waves; ++i) {
+            if (!w[3 * i]) continue;
+            t0 = std::min(t0, w[3 * i]);
+            if (w[3 * i + 1]) e0 = std::min(e0, w[3 * i + 1]);
+        }
+        for (size_t i = 0; i < wt_waves; ++i) {
+            if (!w[3 * i]) continue;
+            starts.push_back((w[3 * i] - t0) * 0.01);  // 100 MHz clock -> us
+            ends.push_back((w[3 * i + 2] - t0) * 0.01);
+        }
+        if (ends.empty()) continue;
+        std::sort(ends.begin(), ends.end());
+        std::sort(starts.begin(), starts.end());
+        auto pct = [](const std::vector<double>& v, double q) { return v[std::min(v.size() - 1, (size_t)(q * v.size()))]; };
+        std::fprintf(stderr, "[wavetime] launch %d waves %zu start p50 %.1f max %.1f | queue empty %.1f | "
+                     "wave end p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f us\n", b, ends.size(), pct(starts, 0.5),
+                     starts.back(), (e0 - t0) * 0.01, pct(ends, 0.1), pct(ends, 0.5), pct(ends, 0.9), pct(ends, 0.99),
+                     ends.back());
+    }
+}
+
 int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed,
-                       const uint32_t* tiles, uint32_t n_tiles, hipStream_t st) {
+                       const uint32_t* tiles, uint32_t n_tiles, hipStream_t st, bool lazy) {
     int rc = set_pixels(h, tiles, n_tiles);
     if (rc) return rc;
     if (h->npix == 0 || n_samples == 0) return RTG_OK;
@@ -1772,14 +1844,19 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     // computeDirectMIS keeps two scratch planes of per-path state in contrib planes 2 and 3
     const int planes = h->integrator == RTG_INTEGRATOR_DIRECT_MIS ? std::max(maxb, 4) : maxb;
     uint32_t ns_chunk = std::max<uint32_t>(1, std::min<uint32_t>(n_samples, h->max_paths / std::max(1u, h->npix)));
+    // the diagnostic modes read one chunk's launches in order on one stream
+    const bool diag = h->timing || h->serial || (RTG_DEBUG && (h->wavetime || h->capture_launch >= 0));
     {
-        // path state of a chunk takes at most half the free HBM (buffers held now count as free)
+        // path state of the chunks in flight takes at most half the free HBM (buffers held now count
+        // as free); pipelined chunks keep RTG_SLOTS sets
         size_t freeb = 0, totalb = 0;
         if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
-            auto path_bytes = [](int pl) { return (size_t)208 + (size_t)16 * (size_t)pl; };
-            const size_t held = h->cap_P * path_bytes(h->cap_maxb);
+            size_t held = 0;
+            for (const ChunkSlot& sl : h->slot) held += slot_bytes(sl);
             const size_t budget = (freeb + held) / 2;
-            const size_t max_ns = budget / path_bytes(planes) / std::max<size_t>(1, h->npix);
+            const size_t per_pix = path_bytes(planes, false) * std::max<size_t>(1, h->npix);
+            size_t max_ns = budget / per_pix;
+            if (!diag && (size_t)ns_chunk * h->npix <= RTG_PIPE_MAX_P) max_ns = budget / RTG_SLOTS / per_pix;
             ns_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(ns_chunk, max_ns));
         }
     }
@@ -1787,7 +1864,8 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     // reading moves between calls, and growing a buffer of ~100 GB means a free and a new
     // hipMalloc that took 5.5 s on C4 with 1G paths in flight.
     {
-        const uint32_t fit = h->cap_maxb >= planes ? (uint32_t)(h->cap_P / std::max(1u, h->npix)) : 0u;
+        const ChunkSlot& s0 = h->slot[0];
+        const uint32_t fit = s0.cap_maxb >= planes ? (uint32_t)(s0.cap_P / std::max(1u, h->npix)) : 0u;
         if (fit >= 1 && ns_chunk > fit && (uint64_t)fit * 4 >= (uint64_t)ns_chunk * 3) ns_chunk = fit;
     }
     // equal chunks: 256 samples at <= 123 per chunk run as 86 + 85 + 85, not 123 + 123 + 10 (a thin
@@ -1797,25 +1875,21 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         ns_chunk = (n_samples + nchunks - 1) / nchunks;
     }
     const size_t P = (size_t)ns_chunk * h->npix;
-    if ((rc = ensure_chunk(h, P, planes))) return rc;
-    if ((rc = ensure_ovf(h))) return rc;
+    // the frame pipeline (rtg_internal.h, ChunkSlot): small chunks rotate through the slots with no
+    // host wait; big ones run in slot 0 with the read-back k_shade grid
+    const bool pipe = !diag && P <= RTG_PIPE_MAX_P;
     (void)hipGetLastError();  // drop any stale error left by other code on this thread
-    HIPOK(hipEventRecord(h->ev[0], st));
+    if (!h->inflight) HIPOK(hipEventRecord(h->ev[0], st));  // start of this render (or of a queued run)
+    HIPOK(hipEventRecord(h->entry, st));  // every chunk starts after the caller's earlier work on st
     std::vector<int> kinds;  // 0 trace, 2 other (timing mode)
     size_t k = 0;
-    PathBufs& pb = h->pb;
     TraceIO io{};
     io.stats = h->d_stats;
     io.cull = h->cull;
     io.wide = h->wide;
-    io.ovf = h->d_ovf;
     // RTG_DEBUG builds with RTG_OPT_WAVETIME: per-wave clocks of chunk 0's trace launches, on stderr
     unsigned long long* d_wt = nullptr;
     const size_t wt_waves = (size_t)std::max(h->trace_blocks, h->trace_blocks_count) * (RTG_TTB / 64);
-    if (RTG_DEBUG && h->wavetime) {
-        HIPOK(hipMalloc((void**)&d_wt, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long)));
-        HIPOK(hipMemsetAsync(d_wt, 0, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long), st));
-    }
     if (h->cap_cnt < maxb + 1) {
         if (h->h_cnt) (void)hipHostFree(h->h_cnt);
         h->h_cnt = nullptr;
@@ -1830,9 +1904,19 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         HIPOK(hipEventCreateWithFlags(&f, hipEventDisableTiming));
         h->sev.push_back(f);
     }
-    if (!h->cstream) HIPOK(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
     uint32_t c = 0;
     for (uint32_t s0 = first; s0 < first + n_samples; s0 += ns_chunk, ++c) {
+        ChunkSlot& sl = pipe ? h->slot[h->next_slot++ % RTG_SLOTS] : h->slot[0];
+        if ((rc = ensure_chunk(h, sl, P, planes, false))) return rc;
+        if ((rc = ensure_ovf(h, sl))) return rc;
+        const hipStream_t ss = sl.stream;
+        PathBufs& pb = sl.pb;
+        io.ovf = sl.d_ovf;
+        HIPOK(hipStreamWaitEvent(ss, h->entry, 0));
+        if (RTG_DEBUG && h->wavetime && c == 0) {
+            HIPOK(hipMalloc((void**)&d_wt, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long)));
+            HIPOK(hipMemsetAsync(d_wt, 0, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long), ss));
+        }
         ChunkArgs a;
         a.pixlist = h->d_pix;
         a.npix = h->npix;
@@ -1845,20 +1929,24 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         a.cam = h->cam;
         a.lean = 1;
         a.seg_tiles = (unsigned)seg_tiles(a.P);
-        HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), st));
-        timed_begin(h, st, k);
-        hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, pb);
+        // k_shade grids from the live counts read back while the traversal runs (big chunks), or over
+        // every tile a segment can hold (blocks past the live count exit at once): no host wait
+        const bool hostgrid = !pipe && (a.seg_tiles >= RTG_HOSTGRID_MIN_TILES || h->serial);
+        if (hostgrid && !h->cstream) HIPOK(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
+        HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), ss));
+        timed_begin(h, ss, k);
+        hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, ss, a, pb);
         LAUNCH_OK("k_generate");
-        timed_end(h, st, k); kinds.push_back(2); ++k;
+        timed_end(h, ss, k); kinds.push_back(2); ++k;
         // Trace launch L_b (b = 0..maxb) carries the extension rays of bounce b (from shade(b-1),
         // or generate) and the shadow rays of bounce b-1: one persistent launch, one drain tail.
         for (int b = 0; b <= maxb; ++b) {
             if (b > 0) {
                 // one 256-path tile per block: 8 x the largest segment's live tiles (the segment
                 // counts of bounce b - 1 arrived while k_trace(b - 1) ran; bounce 0: the camera rays)
-                unsigned tiles = 0;
+                unsigned tiles = hostgrid ? 0u : a.seg_tiles;
                 const unsigned cap = a.seg_tiles * RTG_TB;
-                for (int sgm = 0; sgm < 8; ++sgm) {
+                for (int sgm = 0; hostgrid && sgm < 8; ++sgm) {
                     unsigned live = 0;
                     if (b == 1) {
                         live = a.P > sgm * cap ? std::min(cap, a.P - sgm * cap) : 0u;
@@ -1869,16 +1957,16 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                     tiles = std::max(tiles, (live + RTG_TB - 1) / RTG_TB);
                 }
                 if (tiles) {
-                    timed_begin(h, st, k);
+                    timed_begin(h, ss, k);
                     if (h->integrator == RTG_INTEGRATOR_PATH)
-                        hipLaunchKernelGGL(k_shade<false>, dim3(8 * tiles), dim3(RTG_TB), 0, st, h->sv, a, pb, b - 1);
+                        hipLaunchKernelGGL(k_shade<false>, dim3(8 * tiles), dim3(RTG_TB), 0, ss, h->sv, a, pb, b - 1);
                     else
-                        hipLaunchKernelGGL(k_shade<true>, dim3(8 * tiles), dim3(RTG_TB), 0, st, h->sv, a, pb, b - 1);
+                        hipLaunchKernelGGL(k_shade<true>, dim3(8 * tiles), dim3(RTG_TB), 0, ss, h->sv, a, pb, b - 1);
                     LAUNCH_OK("k_shade");
-                    timed_end(h, st, k); kinds.push_back(2); ++k;
+                    timed_end(h, ss, k); kinds.push_back(2); ++k;
                 }
-                if (b < maxb) {  // the next bounce's segment counts, for its k_shade grid
-                    HIPOK(hipEventRecord(h->sev[b], st));
+                if (hostgrid && b < maxb) {  // the next bounce's segment counts, for its k_shade grid
+                    HIPOK(hipEventRecord(h->sev[b], ss));
                     HIPOK(hipStreamWaitEvent(h->cstream, h->sev[b], 0));
                     HIPOK(hipMemcpyAsync(h->h_cnt + 256 * b, pb.ctr[b].ne8, 256 * sizeof(unsigned),
                                          hipMemcpyDeviceToHost, h->cstream));
@@ -1919,65 +2007,53 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                 HIPOK(hipMalloc((void**)&h->d_cap, cn * (RTG_CAP_LEN / 4) * sizeof(uint4)));
                 HIPOK(hipMalloc((void**)&h->d_cap_len, cn * sizeof(unsigned)));
                 if (!h->d_cap_rays) HIPOK(hipMalloc((void**)&h->d_cap_rays, 35 * sizeof(unsigned)));
-                HIPOK(hipMemsetAsync(h->d_cap_len, 0, cn * sizeof(unsigned), st));
-                hipLaunchKernelGGL(k_cap_slices, dim3(1), dim3(64), 0, st, io, h->d_cap_rays);
+                HIPOK(hipMemsetAsync(h->d_cap_len, 0, cn * sizeof(unsigned), ss));
+                hipLaunchKernelGGL(k_cap_slices, dim3(1), dim3(64), 0, ss, io, h->d_cap_rays);
                 LAUNCH_OK("k_cap_slices");
                 h->cap_n = (unsigned)cn;
                 io.cap = h->d_cap;
                 io.cap_len = h->d_cap_len;
                 io.cap_n = (unsigned)cn;
             }
-            timed_begin(h, st, k);
-            if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TTB), 0, st, h->sv, io);
-            else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, st, h->sv, io);
+            timed_begin(h, ss, k);
+            if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TTB), 0, ss, h->sv, io);
+            else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, ss, h->sv, io);
             LAUNCH_OK("k_trace");
-            timed_end(h, st, k); kinds.push_back(0); ++k;
+            timed_end(h, ss, k); kinds.push_back(0); ++k;
         }
-        hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, st, pb.ctr, maxb, h->d_stats);
+        hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, ss, pb.ctr, maxb, h->d_stats);
         LAUNCH_OK("k_tally");
-        timed_begin(h, st, k);
+        // the film takes the chunks in sample order: this fold runs after the previous chunk's
+        if (h->last_fold) HIPOK(hipStreamWaitEvent(ss, h->last_fold, 0));
+        timed_begin(h, ss, k);
         if (a.ns > 1) {
             const unsigned ppw = a.ns <= 32 ? 64u / (a.ns < 4 ? 4u : a.ns) : 1u;  // pixels per wave (k_accumulate_pm)
             const unsigned waves = (h->npix + ppw - 1) / ppw;
-            hipLaunchKernelGGL(k_accumulate_pm, dim3((waves + RTG_TB / 64 - 1) / (RTG_TB / 64)), dim3(RTG_TB), 0, st, a,
+            hipLaunchKernelGGL(k_accumulate_pm, dim3((waves + RTG_TB / 64 - 1) / (RTG_TB / 64)), dim3(RTG_TB), 0, ss, a,
                                pb, h->d_film);
         } else
-            hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, a, pb, h->d_film);
+            hipLaunchKernelGGL(k_accumulate, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, ss, a, pb, h->d_film);
         LAUNCH_OK("k_accumulate");
-        timed_end(h, st, k); kinds.push_back(2); ++k;
+        timed_end(h, ss, k); kinds.push_back(2); ++k;
+        HIPOK(hipEventRecord(sl.fold, ss));
+        h->last_fold = sl.fold;
+        h->inflight = true;
         h->stats.paths += a.P;
-    }
-    if (d_wt) {
-        std::vector<unsigned long long> wt((size_t)(maxb + 1) * wt_waves * 3);
-        HIPOK(hipStreamSynchronize(st));
-        HIPOK(hipMemcpy(wt.data(), d_wt, wt.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-        (void)hipFree(d_wt);
-        for (int b = 0; b <= maxb; ++b) {
-            const unsigned long long* w = wt.data() + (size_t)b * wt_waves * 3;
-            unsigned long long t0 = ~0ull, e0 = ~0ull;
-            std::vector<double> ends, starts;
-            for (size_t i = 0; i < wt_waves; ++i) {
-                if (!w[3 * i]) continue;
-                t0 = std::min(t0, w[3 * i]);
-                if (w[3 * i + 1]) e0 = std::min(e0, w[3 * i + 1]);
-            }
-            for (size_t i = 0; i < wt_waves; ++i) {
-                if (!w[3 * i]) continue;
-                starts.push_back((w[3 * i] - t0) * 0.01);  // 100 MHz clock -> us
-                ends.push_back((w[3 * i + 2] - t0) * 0.01);
-            }
-            if (ends.empty()) continue;
-            std::sort(ends.begin(), ends.end());
-            std::sort(starts.begin(), starts.end());
-            auto pct = [](const std::vector<double>& v, double q) { return v[std::min(v.size() - 1, (size_t)(q * v.size()))]; };
-            std::fprintf(stderr, "[wavetime] launch %d waves %zu start p50 %.1f max %.1f | queue empty %.1f | "
-                         "wave end p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f us\n", b, ends.size(), pct(starts, 0.5),
-                         starts.back(), (e0 - t0) * 0.01, pct(ends, 0.1), pct(ends, 0.5), pct(ends, 0.9), pct(ends, 0.99),
-                         ends.back());
+        if (d_wt) {
+            std::vector<unsigned long long> wt((size_t)(maxb + 1) * wt_waves * 3);
+            HIPOK(hipStreamSynchronize(ss));
+            HIPOK(hipMemcpy(wt.data(), d_wt, wt.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+            (void)hipFree(d_wt);
+            d_wt = nullptr;
+            print_wavetime(wt, maxb, wt_waves);
         }
     }
-    HIPOK(hipEventRecord(h->ev[1], st));
     h->spp += n_samples;
+    if (lazy) return RTG_OK;
+    // the caller's stream waits for the chunks (and for every chunk queued before them)
+    h->inflight = false;
+    HIPOK(hipStreamWaitEvent(st, h->last_fold, 0));
+    HIPOK(hipEventRecord(h->ev[1], st));
     if (h->timing) {
         HIPOK(hipEventSynchronize(h->ev[1]));
         h->stats.extend_ms = h->stats.shadow_ms = h->stats.shade_ms = 0;
@@ -2003,19 +2079,39 @@ int rtg_render_async(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, c
     if (!h) { g_err = "null handle"; return RTG_ERR_ARG; }
     HIPOK(hipSetDevice(h->device));
     hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    return render_impl(h, first, n, seed, tiles, n_tiles, st);
+    return render_impl(h, first, n, seed, tiles, n_tiles, st, stream == nullptr);
 }
 
 int rtg_render(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, const uint32_t* tiles, uint32_t n_tiles) {
-    int rc = rtg_render_async(h, first, n, seed, tiles, n_tiles, nullptr);
+    if (!h) { g_err = "null handle"; return RTG_ERR_ARG; }
+    HIPOK(hipSetDevice(h->device));
+    int rc = render_impl(h, first, n, seed, tiles, n_tiles, h->stream, false);
     if (rc) return rc;
     return rtg_synchronize(h);
+}
+
+int rtg_render_idle(rtg_handle* h, int* idle) {
+    if (!h || !idle) { g_err = "rtg_render_idle: null argument"; return RTG_ERR_ARG; }
+    HIPOK(hipSetDevice(h->device));
+    *idle = 1;
+    if (h->last_fold) {
+        const hipError_t e = hipEventQuery(h->last_fold);
+        if (e == hipErrorNotReady) *idle = 0;
+        else if (e != hipSuccess) { g_err = std::string("rtg_render_idle: ") + hipGetErrorString(e); return RTG_ERR_HIP; }
+    }
+    if (*idle) {
+        const hipError_t e = hipStreamQuery(h->stream);
+        if (e == hipErrorNotReady) *idle = 0;
+        else if (e != hipSuccess) { g_err = std::string("rtg_render_idle: ") + hipGetErrorString(e); return RTG_ERR_HIP; }
+    }
+    return RTG_OK;
 }
 
 int rtg_render_adaptive(rtg_handle* h, uint32_t first, uint64_t seed, uint32_t init_samples, uint32_t max_samples,
                         uint32_t min_samples, uint32_t* tile_samples) {
     if (!h || init_samples == 0) { g_err = "rtg_render_adaptive: bad argument"; return RTG_ERR_ARG; }
     HIPOK(hipSetDevice(h->device));
+    if (int rc0 = join_frames(h)) return rc0;
     hipStream_t st = h->stream;
     const size_t nf = (size_t)h->W * h->H * 3;
     const uint32_t spp0 = h->spp;
@@ -2028,7 +2124,7 @@ int rtg_render_adaptive(rtg_handle* h, uint32_t first, uint64_t seed, uint32_t i
     // ---- pass 1 (adaptiveSampling, Renderer.h:583-638): per-pixel sums of init_samples samples
     h->d_film = d_tmp;
     if (hipMemsetAsync(d_tmp, 0, nf * sizeof(float), st) != hipSuccess) return fail(RTG_ERR_HIP);
-    int rc = render_impl(h, first, init_samples, seed, nullptr, 0, st);
+    int rc = render_impl(h, first, init_samples, seed, nullptr, 0, st, false);
     if (rc) return fail(rc);
     std::vector<float> sums(nf);
     if (hipStreamSynchronize(st) != hipSuccess ||
@@ -2091,7 +2187,7 @@ int rtg_render_adaptive(rtg_handle* h, uint32_t first, uint64_t seed, uint32_t i
         if (n == 0) continue;
         h->d_film = d_tmp;
         if (hipMemsetAsync(d_tmp, 0, nf * sizeof(float), st) != hipSuccess) return fail2(RTG_ERR_HIP);
-        if ((rc = render_impl(h, first + init_samples, n, seed, group.data(), (uint32_t)group.size(), st))) return fail2(rc);
+        if ((rc = render_impl(h, first + init_samples, n, seed, group.data(), (uint32_t)group.size(), st, false))) return fail2(rc);
         h->d_film = d_keep;
         hipLaunchKernelGGL(k_fold_mean, dim3((h->npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, st, h->d_pix, h->npix,
                            (const float*)d_tmp, (float)n, d_acc);
@@ -2125,6 +2221,7 @@ int rtg_debug_replay(rtg_handle* h, double* out) {
 #if RTG_DEBUG
     if (!h->d_cap) { g_err = "rtg_debug_replay: nothing captured"; return RTG_ERR_ARG; }
     HIPOK(hipSetDevice(h->device));
+    if (int rc = join_frames(h)) return rc;
     HIPOK(hipStreamSynchronize(h->stream));
     unsigned tab[35];
     HIPOK(hipMemcpy(tab, h->d_cap_rays, sizeof(tab), hipMemcpyDeviceToHost));
@@ -2173,6 +2270,8 @@ int rtg_debug_replay(rtg_handle* h, double* out) {
 
 int rtg_synchronize(rtg_handle* h) {
     if (!h) return RTG_ERR_ARG;
+    HIPOK(hipSetDevice(h->device));
+    if (int rc = join_frames(h)) return rc;
     HIPOK(hipStreamSynchronize(h->stream));
     float ms = 0;
     if (hipEventElapsedTime(&ms, h->ev[0], h->ev[1]) == hipSuccess) h->stats.render_ms = ms;
@@ -2182,6 +2281,11 @@ int rtg_synchronize(rtg_handle* h) {
 int rtg_film_read(rtg_handle* h, float* rgb, uint32_t* spp) {
     if (!h) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
+    if (!rgb) {  // Film::SPP only: counts queued frames, waits for nothing
+        if (spp) *spp = h->spp;
+        return RTG_OK;
+    }
+    if (int rc = join_frames(h)) return rc;
     HIPOK(hipStreamSynchronize(h->stream));
     if (rgb) HIPOK(hipMemcpy(rgb, h->d_film, (size_t)h->W * h->H * 3 * sizeof(float), hipMemcpyDeviceToHost));
     if (spp) *spp = h->spp;
@@ -2191,6 +2295,7 @@ int rtg_film_read(rtg_handle* h, float* rgb, uint32_t* spp) {
 int rtg_film_copy_device(rtg_handle* h, void* dst) {
     if (!h || !dst) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
+    if (int rc = join_frames(h)) return rc;
     HIPOK(hipMemcpyAsync(dst, h->d_film, (size_t)h->W * h->H * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->stream));
     HIPOK(hipStreamSynchronize(h->stream));
     return RTG_OK;
@@ -2199,6 +2304,8 @@ int rtg_film_copy_device(rtg_handle* h, void* dst) {
 int rtg_film_load(rtg_handle* h, const float* rgb, uint32_t spp) {
     if (!h || !rgb) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
+    if (int rc = join_frames(h)) return rc;
+    HIPOK(hipStreamSynchronize(h->stream));  // (hipMemcpy does not order against non-blocking streams)
     HIPOK(hipMemcpy(h->d_film, rgb, (size_t)h->W * h->H * 3 * sizeof(float), hipMemcpyHostToDevice));
     h->spp = spp;
     return RTG_OK;
@@ -2207,6 +2314,7 @@ int rtg_film_load(rtg_handle* h, const float* rgb, uint32_t spp) {
 int rtg_clear(rtg_handle* h) {
     if (!h) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
+    if (int rc = join_frames(h)) return rc;
     HIPOK(hipMemsetAsync(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float), h->stream));
     HIPOK(hipMemsetAsync(h->d_stats, 0, 16 * sizeof(unsigned long long), h->stream));
     HIPOK(hipStreamSynchronize(h->stream));
@@ -2218,6 +2326,7 @@ int rtg_clear(rtg_handle* h) {
 int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     if (!h || !out) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
+    if (int rc = join_frames(h)) return rc;
     HIPOK(hipStreamSynchronize(h->stream));
     unsigned long long c[16] = {};
     HIPOK(hipMemcpy(c, h->d_stats, sizeof(c), hipMemcpyDeviceToHost));
@@ -2243,6 +2352,8 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
     if (!h || !rays || (!hits && !vis)) return RTG_ERR_ARG;
     if (n == 0) return RTG_OK;
     HIPOK(hipSetDevice(h->device));
+    if (int rc = join_frames(h)) return rc;
+    HIPOK(hipStreamSynchronize(h->stream));  // slot 0's overflow stack is free (hipMemcpy below)
     // path-id indirection of the trace kernels: identity queue over n query rays
     float4 *d_o = nullptr, *d_d = nullptr;
     unsigned* d_q = nullptr;
@@ -2266,11 +2377,12 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
     }
     unsigned hc[4] = {n, 0, 0, 0};
     HIPOK(hipMemcpy(h->d_qctr, hc, sizeof(hc), hipMemcpyHostToDevice));
-    int rc = ensure_ovf(h);
+    int rc = ensure_ovf(h, h->slot[0]);
     if (rc) return rc;
+    if (h->slot[0].stream) HIPOK(hipStreamSynchronize(h->slot[0].stream));
     TraceIO io{};
     io.fetch = h->d_qctr + 1;
-    io.ovf = h->d_ovf;
+    io.ovf = h->slot[0].d_ovf;
     io.stats = h->d_stats;
     io.cull = h->cull;
     io.wide = h->wide;

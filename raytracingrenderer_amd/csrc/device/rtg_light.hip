@@ -482,7 +482,7 @@ static int trace_light_paths(rtg_handle* h, hipStream_t st, LightArgs& a, PathBu
     io.stats = h->d_stats;
     io.cull = h->cull;
     io.wide = h->wide;
-    io.ovf = h->d_ovf;
+    io.ovf = h->slot[0].d_ovf;
     io.ray_o = pb.ray_o;
     io.ray_d = pb.ray_d;
     io.hits = pb.hits;
@@ -540,8 +540,10 @@ int rtg_render_light(rtg_handle* h, uint32_t first, uint32_t n_frames, uint64_t 
     if ((uint64_t)first + n_frames > 65536u) { g_err = "frame index >= 65536 (PCG stream key)"; return RTG_ERR_ARG; }
     const size_t P = std::min<size_t>(npaths, h->max_paths);
     int rc;
-    if ((rc = ensure_chunk(h, P, std::max(h->cap_maxb, 1)))) return rc;
-    if ((rc = ensure_ovf(h))) return rc;
+    if ((rc = join_frames(h))) return rc;
+    HIPOK(hipStreamSynchronize(st));  // slot 0's buffers are free
+    if ((rc = ensure_chunk(h, h->slot[0], P, std::max(h->slot[0].cap_maxb, 1), true))) return rc;
+    if ((rc = ensure_ovf(h, h->slot[0]))) return rc;
     // records: at most one per path and vertex; grown on demand
     size_t cap = 4 * P + 1024;
     DevBuf key, col, key2, idx, idx2, rn, tmp;
@@ -549,7 +551,7 @@ int rtg_render_light(rtg_handle* h, uint32_t first, uint32_t n_frames, uint64_t 
     DALLOC(rn, 16);
     size_t tmp_bytes = 0;
     const DevProj cam = make_proj(h);
-    PathBufs& pb = h->pb;
+    PathBufs& pb = h->slot[0].pb;
     for (uint32_t f = first; f < first + n_frames; ++f) {
         for (size_t base = 0; base < npaths; base += P) {
             LightArgs a{};
@@ -603,11 +605,13 @@ int rtg_render_instant_radiosity(rtg_handle* h, uint32_t first, uint32_t n_frame
     hipStream_t st = h->stream;
     if ((uint64_t)first + n_frames > 65536u) { g_err = "frame index >= 65536 (PCG stream key)"; return RTG_ERR_ARG; }
     int rc;
+    if ((rc = join_frames(h))) return rc;
+    HIPOK(hipStreamSynchronize(st));  // slot 0's buffers are free
     if ((rc = set_pixels(h, nullptr, 0))) return rc;
     const unsigned npix = h->npix;
-    if ((rc = ensure_chunk(h, std::max<size_t>(npix, n_vpl), std::max(h->cap_maxb, 1)))) return rc;
-    if ((rc = ensure_ovf(h))) return rc;
-    PathBufs& pb = h->pb;
+    if ((rc = ensure_chunk(h, h->slot[0], std::max<size_t>(npix, n_vpl), std::max(h->slot[0].cap_maxb, 1), true))) return rc;
+    if ((rc = ensure_ovf(h, h->slot[0]))) return rc;
+    PathBufs& pb = h->slot[0].pb;
     const DevProj cam = make_proj(h);
     size_t cap = 64 * (size_t)n_vpl + 1024;
     DevBuf vkey, vrec, rn, px, pn, pf, acc, vpl_d;
@@ -668,7 +672,7 @@ int rtg_render_instant_radiosity(rtg_handle* h, uint32_t first, uint32_t n_frame
         io.stats = h->d_stats;
         io.cull = h->cull;
         io.wide = h->wide;
-        io.ovf = h->d_ovf;
+        io.ovf = h->slot[0].d_ovf;
         io.queue = pb.q[0];
         io.ray_o = pb.ray_o;
         io.ray_d = pb.ray_d;
@@ -700,7 +704,7 @@ int rtg_render_instant_radiosity(rtg_handle* h, uint32_t first, uint32_t n_frame
                 sio.stats = h->d_stats;
                 sio.cull = h->cull;
                 sio.wide = h->wide;
-                sio.ovf = h->d_ovf;
+                sio.ovf = h->slot[0].d_ovf;
                 sio.squeue = q.get<unsigned>();
                 sio.sray_o = so.get<float4>();
                 sio.sray_d = sd.get<float4>();

@@ -211,7 +211,9 @@ class RayTracer:
         return (self.height + 31) // 32
 
     def render(self, n_samples=1, tiles=None, first_sample=None, sync=True):
-        """RayTracer::render(): add n_samples samples per pixel (default 1 = one frame)."""
+        """RayTracer::render(): add n_samples samples per pixel (default 1 = one frame).
+        sync=False queues the frame (rtg_render_async): a frame loop of 1-spp calls then keeps up to
+        three frames in flight on the GPU; film() / stats() / synchronize() wait for them."""
         first = self.getSPP() if first_sample is None else first_sample
         t = None if tiles is None else np.ascontiguousarray(tiles, np.uint32)
         tp = N.ptr(t, C.c_uint32) if t is not None else None
@@ -253,6 +255,12 @@ class RayTracer:
 
     def synchronize(self):
         _check(self._lib.rtg_synchronize(self._h), self._lib.rtg_last_error)
+
+    def idle(self):
+        """True when no queued render work is left on the GPU (rtg_render_idle)."""
+        v = C.c_int()
+        _check(self._lib.rtg_render_idle(self._h, C.byref(v)), self._lib.rtg_last_error)
+        return bool(v.value)
 
     def film(self):
         """(sum, spp): the unnormalised Film::film and Film::SPP."""

@@ -29,6 +29,7 @@ SCENES = {
     "synth20k": ("/tmp/rtg_golden_synth20k", 0, 0, False),
     "coffee_f": (os.path.join(REF, "coffee"), 400, 500, True),
     "bathroom_f": (os.path.join(REF, "bathroom"), 480, 270, True),
+    "materialball_f": (os.path.join(REF, "materialball"), 320, 180, True),
 }
 ARRAYS = ("positions", "normals", "uvs", "material", "node_bounds", "node_links", "lights", "camera")
 
@@ -165,6 +166,37 @@ def synth1m_digests():
     json.dump(dg, open(os.path.join(GOLD, "scene_digests.json"), "w"), indent=1, sort_keys=True)
 
 
+def add_scene_digests(names):
+    """Loader + BVH digests of the listed SCENES entries only, merged into scene_digests.json (the
+    other entries are left as they are)."""
+    dg = json.load(open(os.path.join(GOLD, "scene_digests.json")))
+    for name in names:
+        path, w, h, skip = SCENES[name]
+        r = pyref.RefScene(path, w, h, skip)
+        d = r.export()
+        dg[name] = {k: digest(d[k]) for k in ARRAYS}
+        dg[name].update(n_tris=r.ntri, n_nodes=r.nnode, n_lights=r.nlight, width=r.W, height=r.H,
+                        mat_info=digest(d["mat_info"][:, :2]), mat_f=digest(d["mat_f"]))
+    json.dump(dg, open(os.path.join(GOLD, "scene_digests.json"), "w"), indent=1, sort_keys=True)
+
+
+def rtm_digest_fixture(stride=127):
+    """include/rtg_math.h's own outputs (no C library call) on every stride-th float and 2^20 atan2f
+    pairs, as FNV-1a digests, with the platform they were checked on (glibc 2.35, FMA build: the
+    exhaustive match of profiles/r03_libm_exhaustive.txt) -> rtm_digest.json. The CPU suite then
+    pins the restatement itself on any host, and compares with the host's C library only where that
+    library is the reference platform's."""
+    import subprocess
+    from oracle.pyoracle import BUILD
+    out = subprocess.run([os.path.join(BUILD, "libm_check"), "digest", str(stride)], capture_output=True, text=True,
+                         check=True).stdout.split()
+    # "glibc 2.35 fma 1 avx2 1" / "stride N sinf H cosf H ..."
+    plat = dict(zip(out[0:6:2], out[1:6:2]))
+    dig = dict(zip(out[6::2], out[7::2]))
+    json.dump({"platform": plat, "digests": dig, "command": "oracle/_build/libm_check digest %d" % stride},
+              open(os.path.join(GOLD, "rtm_digest.json"), "w"), indent=1, sort_keys=True)
+
+
 def tonemap_fixture():
     """Film::tonemap (Imaging.h:233-242) of the reference's own Film class on a random film with
     negative, zero, tiny, saturating and non-finite values, at two exposures -> tonemap_kat.npz."""
@@ -184,6 +216,10 @@ if __name__ == "__main__":
         light_fixtures()
     elif "--synth1m" in sys.argv:
         synth1m_digests()
+    elif "--rtm-digest" in sys.argv:
+        rtm_digest_fixture()
+    elif "--materialball" in sys.argv:
+        add_scene_digests(["materialball_f"])
     elif "--tonemap" in sys.argv:
         tonemap_fixture()
     else:

@@ -31,7 +31,7 @@ def test_exports_cover_header(header, lib):
 
 
 def test_abi_version():
-    assert N.rtg().rtg_abi_version() == 3
+    assert N.rtg().rtg_abi_version() == 4
 
 
 def test_no_gpu_fails_loudly():

@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLD, SCENES, scene_path
+from conftest import GOLD, SCENES, require_reference_libm, scene_path
 from oracle.pyoracle import Oracle
 from raytracingrenderer_amd import RayTracer, loadScene, write_synthetic_scene
 from raytracingrenderer_amd import _native as N
@@ -170,16 +170,60 @@ def test_tiles_and_chunks_compose(cornell256):
     assert_bitexact(rt4.film()[0], full, "resume")
 
 
+@pytest.mark.parametrize("serial", [False, True])
 @pytest.mark.parametrize("w,h,spp,max_paths", [(1, 1, 1, 0), (17, 15, 1, 0), (16, 16, 1, 0), (33, 31, 3, 0),
                                                (64, 35, 2, 0), (33, 31, 3, 300)])
-def test_queue_segment_edges(w, h, spp, max_paths):
-    """Segmented queues (8 segments of ceil(ceil(P / 256) / 8) tiles each; k_shade's grid from the
-    read-back counts): P = 1 (seven empty segments), 255, 256, 3069 and 4480 paths, and chunks of at
-    most 300 paths, at depth 8 so later bounces empty whole segments: bit-exact vs the oracle."""
+def test_queue_segment_edges(w, h, spp, max_paths, serial):
+    """Segmented queues (8 segments of ceil(ceil(P / 256) / 8) tiles each): P = 1 (seven empty
+    segments), 255, 256, 3069 and 4480 paths, and chunks of at most 300 paths, at depth 8 so later
+    bounces empty whole segments: bit-exact vs the oracle. Both k_shade grid sizings: every tile a
+    segment can hold, chunks rotating through the frame pipeline's slots (default for chunks of <= 8M
+    paths), and the live tiles from the read-back counts, one chunk at a time (RTG_OPT_SERIAL, the
+    sizing of big chunks)."""
     s = loadScene(os.path.join(SCENES, "cornell-mat"), width=w, height=h)
-    film = gpu_film(s, spp, seed=7, max_depth=8, max_paths=max_paths)
+    rt = RayTracer(s, seed=7, max_depth=8, max_paths=max_paths)
+    if serial:
+        rt.set_options(flags=rt.flags | N.RTG_OPT_SERIAL)
+    rt.render(spp, first_sample=0)
+    film = rt.film()[0]
     ref, _ = Oracle(s, 8, "rtm").render(spp, seed=7, threads=8)
     assert_bitexact(film, ref, "%dx%d x%d spp, max_paths %d" % (w, h, spp, max_paths))
+
+
+def test_queued_frames_return_early_and_equal_one_render(tmp_path):
+    """The drop-in frame loop (Main.cpp:74-118: one RayTracer::render() per frame): 1-spp
+    rtg_render_async calls are queued with no host wait and return before their work has run; up to
+    three frames run side by side, and the film, folded in sample order, is bit-identical to one
+    rtg_render of all the samples. Film::SPP is readable at once; a film read waits for the frames."""
+    d = str(tmp_path / "s")
+    write_synthetic_scene(d, n_tris=200000, seed=5, width=1024, height=1024)
+    s = loadScene(d)
+    full = gpu_film(s, 12, seed=99)
+    rt = RayTracer(s, seed=99)
+    rt.render(1, sync=False)  # warm: buffers of the first slots
+    rt.clear()
+    rt.synchronize()
+    assert rt.idle()
+    for f in range(12):
+        rt.render(1, first_sample=f, sync=False)
+        if f == 0:
+            # a 1M-path frame of a 200k-triangle scene runs for milliseconds; the call returned at once
+            assert not rt.idle(), "rtg_render_async waited for its frame"
+    assert rt.getSPP() == 12
+    film, spp = rt.film()
+    assert spp == 12 and rt.idle()
+    assert_bitexact(film, full, "12 queued 1-spp frames vs one 12-spp render")
+    # queued frames, a synchronous render and tile subsets interleaved; a clear in between
+    rt.clear()
+    tiles = np.arange(rt.tiles_x * rt.tiles_y, dtype=np.uint32)
+    for f in range(0, 12, 3):
+        rt.render(1, first_sample=f, sync=False)
+        rt.render(1, first_sample=f + 1, tiles=tiles[::2], sync=False)
+        rt.render(1, first_sample=f + 1, tiles=tiles[1::2], sync=False)
+        rt.render(1, first_sample=f + 2, sync=True)
+    assert_bitexact(rt.film()[0], full, "interleaved queued / tiled / synchronous frames")
+    st = rt.stats()
+    assert st["paths"] == 12 * 1024 * 1024
 
 
 @pytest.mark.parametrize("name", ["cornell256", "synth20k"])
@@ -483,6 +527,8 @@ def test_gpu_film_vs_reference_classes(case, flavour, synth20k):
     bit: a film-level pin that does not go through the C oracle. libref.so calls the C library's
     transcendentals (the reference as built on Linux); libref_rtm.so has include/rtg_math.h's
     interposed (the same bits, which is what this shows at the film level)."""
+    if flavour == "libm":
+        require_reference_libm()
     from oracle import pyref
     if not pyref.available():
         pytest.fail("oracle/_ref (libref_rtm.so) missing: build it where /root/reference exists")
@@ -510,6 +556,7 @@ def _nan_canon(a):
     return np.where(np.isnan(a), np.float32(np.nan), a).view(np.uint32)
 
 
+@pytest.mark.host_glibc
 def test_device_math_matches_glibc():
     """The kernels' transcendentals (include/rtg_math.h compiled for gfx950, rtg_probe_math) against
     the host C library (liboracle_libm's or_math_eval calls glibc), bit for bit (any NaN equals any
@@ -566,16 +613,18 @@ def test_gpu_integrators_vs_reference_classes(scene_name):
     assert_bitexact(rt.film()[0], fa, "adaptive")
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C4", "C5"])
+@pytest.mark.parametrize("cfg", ["C2", "C4", "C5", "MB"])
 def test_full_size_configs_sampled_pixels(cfg):
     """BASELINE.json's other configs at their full sizes, rendered as the bench renders them (one
     rtg_render call of every sample: wavefront chunks, pixel-major fold): sampled pixels equal the
     oracle's per-path radiances summed in sample order, bit for bit.
     C2 cornell 1024^2 x 64 spp depth 8; C4 bathroom_f 1920x1080 x 256 spp depth 16; C5 coffee_f +
-    GI.hdr 4096^2 x 1024 spp depth 4 (17.2G paths, ~7.5 s on one MI355X)."""
+    GI.hdr 4096^2 x 1024 spp depth 4 (17.2G paths, ~7.5 s on one MI355X); MB: materialball_f at its
+    own 1280x720, 64 spp, depth 8 (envmap.hdr is lights[0])."""
     spec = {"C2": ("cornell-box", 1024, 1024, 64, 8, {}, 4000),
             "C4": ("bathroom", 1920, 1080, 256, 16, {"skip_missing": True}, 1500),
-            "C5": ("coffee", 4096, 4096, 1024, 4, {"skip_missing": True, "envmap": "GI.hdr"}, 1000)}[cfg]
+            "C5": ("coffee", 4096, 4096, 1024, 4, {"skip_missing": True, "envmap": "GI.hdr"}, 1000),
+            "MB": ("materialball", 1280, 720, 64, 8, {"skip_missing": True}, 2000)}[cfg]
     name, w, h, spp, depth, kw, npix = spec
     path = os.path.join(SCENES, name) if name == "cornell-box" else staged(name)
     s = loadScene(path, width=w, height=h, **kw)
@@ -607,7 +656,8 @@ def test_count_mode_counters_are_consistent(synth20k, cornell256):
         assert s["node_lane_steps"] > 0 and s["extension_rays"] > 0, s
 
 
-@pytest.mark.parametrize("case", ["cornell-mat", "bathroom", "coffee+GI"])
+@pytest.mark.host_glibc
+@pytest.mark.parametrize("case", ["cornell-mat", "bathroom", "coffee+GI", "materialball"])
 def test_reference_side_binding_renders_reference_film(case):
     """The drop-in from the reference side: RTBase's own loader builds the Scene (oracle/_ref, the
     reference headers), integration/rtg_rtbase.h flattens it (the code INTEGRATION.md §2 shows),
@@ -620,6 +670,7 @@ def test_reference_side_binding_renders_reference_film(case):
         "cornell-mat": (os.path.join(SCENES, "cornell-mat"), dict(width=80, height=60), 8, 3, 21),
         "bathroom": (staged("bathroom"), dict(width=96, height=54, skip_missing=True), 16, 2, 22),
         "coffee+GI": (staged("coffee"), dict(width=80, height=100, skip_missing=True, envmap="GI.hdr"), 4, 3, 23),
+        "materialball": (staged("materialball"), dict(width=96, height=54, skip_missing=True), 8, 2, 24),
     }[case]
     r = pyref.RefScene(path, kw["width"], kw["height"], kw.get("skip_missing", False), kw.get("envmap"),
                        flavour="libm")

@@ -54,14 +54,17 @@ def test_synthetic_scene_matches_reference_loader(tmp_path):
     _check_digests("synth20k", loadScene(str(tmp_path)))
 
 
-@pytest.mark.parametrize("name,dirname,w,h", [("coffee_f", "coffee", 400, 500), ("bathroom_f", "bathroom", 480, 270)])
+@pytest.mark.parametrize("name,dirname,w,h", [("coffee_f", "coffee", 400, 500), ("bathroom_f", "bathroom", 480, 270),
+                                             ("materialball_f", "materialball", 320, 180)])
 def test_filtered_scenes_match_reference_loader(name, dirname, w, h):
     p = scene_path(dirname)
     if p is None:
         pytest.skip("scene assets not available here")
     s = loadScene(p, width=w, height=h, skip_missing=True)
     _check_digests(name, s)
-    assert s.info.dropped_instances == {"coffee_f": 3, "bathroom_f": 4}[name]
+    assert s.info.dropped_instances == {"coffee_f": 3, "bathroom_f": 4, "materialball_f": 1}[name]
+    if name == "materialball_f":  # the environment is the scene's only light (lights[0] = env: -1)
+        assert s.info.env_in_lights == 1 and list(s.lights) == [-1]
 
 
 def test_synthetic_generator_deterministic(tmp_path):

@@ -6,11 +6,14 @@ The full check runs every 2^32 float input through oracle/libm_check (profiles/r
 the CPU suite repeats it on every 31st input and on 2^24 atan2 pairs, against the C library of the
 machine the tests run on."""
 import ctypes as C
+import json
 import os
 import subprocess
 
 import numpy as np
+import pytest
 
+from conftest import GOLD
 from oracle.pyoracle import BUILD, lib
 
 CHECK = os.path.join(BUILD, "libm_check")
@@ -25,6 +28,19 @@ def _run_check(*args):
     return lines
 
 
+def test_restatement_digest_is_pinned():
+    """include/rtg_math.h's own outputs (no C library involved, so on any host) on every 127th float
+    and 2^20 atan2f pairs equal the digests recorded where they matched glibc 2.35's FMA build bit
+    for bit on every input (tests/golden/rtm_digest.json, profiles/r03_libm_exhaustive.txt)."""
+    want = json.load(open(os.path.join(GOLD, "rtm_digest.json")))
+    r = subprocess.run([CHECK, "digest", want["digests"]["stride"]], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    got = r.stdout.split()
+    assert dict(zip(got[6::2], got[7::2])) == want["digests"]
+    assert want["platform"] == {"glibc": "2.35", "fma": "1", "avx2": "1"}
+
+
+@pytest.mark.host_glibc
 def test_unary_functions_equal_glibc_on_every_31st_float():
     """sinf, cosf, sincosf (and glibc's sincosf against its own sinf/cosf, so a compiler that fuses
     the reference's sin/cos pairs changes nothing) and acosf: 138.5M inputs spread over all
@@ -33,6 +49,7 @@ def test_unary_functions_equal_glibc_on_every_31st_float():
     assert any(l.startswith("acosf") for l in lines) and any(l.startswith("sincosf.cos") for l in lines)
 
 
+@pytest.mark.host_glibc
 def test_atan2_equals_glibc_on_structured_pairs():
     """atan2f on 2^24 pairs: random bit patterns, unit-vector components (EnvironmentMap::evaluate's
     inputs), close exponents, x = +-1 (glibc's atanf shortcut) and every special operand."""
@@ -52,6 +69,7 @@ def same_bits(a, b):
                           np.where(np.isnan(b), np.float32(np.nan), b).view(np.uint32))
 
 
+@pytest.mark.host_glibc
 def test_oracle_flavours_agree_on_the_sampled_directions():
     """The oracle's two builds (liboracle_rtm: include/rtg_math.h, liboracle_libm: the C library)
     on the path's actual arguments: theta = acosf(sqrt(r1)), acosf(1 - 2 r1), phi = 2 pi r2 and
@@ -69,6 +87,7 @@ def test_oracle_flavours_agree_on_the_sampled_directions():
     assert same_bits(_eval("rtm", 4, yx, len(d)), _eval("libm", 4, yx, len(d)))
 
 
+@pytest.mark.host_glibc
 def test_special_cases():
     L, G = lib("rtm"), lib("libm")
     for v in (0.0, -0.0, 1.0, -1.0, 0.5, -0.5, 1.0000001, -1.0000001, 1e-30, -1e-30, 2 ** -26, 120.0, -120.0,

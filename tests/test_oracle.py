@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLD, REF_ROOT, SCENES
+from conftest import GOLD, REF_ROOT, SCENES, require_reference_libm
 from oracle.pyoracle import Oracle
 from raytracingrenderer_amd import loadScene, read_hdr
 
@@ -24,6 +24,7 @@ def md5(img):
     return hashlib.md5(np.ascontiguousarray(img, np.float32).tobytes()).hexdigest()
 
 
+@pytest.mark.host_glibc
 def test_c1_known_answer_glibc(cornell256):
     """cornell 256^2 x 4 spp, depth 4, PCG seed 1234 -> md5 2fe4126e... (glibc 2.35)."""
     kat = FILM_KAT["C1_libm"]
@@ -148,6 +149,9 @@ REF_FILM_CASES = [
     ("cornell-mat", dict(width=80, height=60), 8, 3, 99),
     ("bathroom", dict(width=96, height=54, skip_missing=True), 16, 2, 7),
     ("coffee", dict(width=80, height=100, skip_missing=True, envmap="GI.hdr"), 4, 3, 5),
+    # the one reference scene whose environment map is a light (lights[0], Scene.h:156-159;
+    # EnvironmentMap, Lights.h:135-201): materialball_f (Mesh002.gem is missing)
+    ("materialball", dict(width=96, height=54, skip_missing=True), 8, 2, 13),
 ]
 
 
@@ -166,6 +170,8 @@ def test_oracle_film_equals_reference_classes(case, flavour):
     classes (ref_render: Scene::traverse/visible, calculateShadingData, BSDF::sample/evaluate,
     Light::sample, Camera, Film::splat from /root/reference), with glibc and with the shared
     transcendentals: films identical bit for bit, and the same closest-hit / shadow ray counts."""
+    if flavour == "libm":
+        require_reference_libm()
     from oracle import pyref
     if not pyref.available():
         pytest.skip("oracle/_ref not built")
@@ -179,6 +185,7 @@ def test_oracle_film_equals_reference_classes(case, flavour):
     assert rc.tolist() == oc[:3].tolist()
 
 
+@pytest.mark.host_glibc
 def test_c1_known_answer_from_reference_classes():
     """SURVEY.md §8c's C1 md5 (the reference integrator built in the survey, glibc) is reproduced by
     ref_render on the reference's own classes, so both the oracle and ref_render are pinned to it."""
@@ -191,6 +198,7 @@ def test_c1_known_answer_from_reference_classes():
     assert c.tolist() == [262144, 702961, 429793]
 
 
+@pytest.mark.host_glibc
 @pytest.mark.parametrize("scene_name", ["cornell-box", "cornell-mat"])
 def test_oracle_integrators_equal_reference_classes(scene_name):
     """f4: every alternative integrator of the oracle (direct, albedo, viewNormals, computeDirectMIS,
