@@ -286,9 +286,10 @@ def main():
     elapsed = time.perf_counter() - t_start
 
     # the drop-in frame loop (Main.cpp:74-118): one RayTracer::render() = one rtg call of 1 spp
+    # (without the per-launch timing events, which keep one chunk in flight)
     dropin = None
     if world == 1 and group_devs is None and a.dropin_frames > 0:
-        dropin = dropin_leg(rt, a, tiles)
+        dropin = dropin_leg(rt, a, tiles, base)
 
     # counting passes (untimed): box / triangle tests per closest-hit ray on the same workload.
     # Algorithmic work is the reference's BVH2 walk; the 4-wide walk's own tests are reported too.
@@ -331,6 +332,15 @@ def main():
                       "reduce_ms_per_step": round(float(np.mean(timed_reduce)), 3) if timed_reduce else None,
                       "rank_kernel_ms_last_step": [{"trace": round(r["extend_ms"], 2), "shade": round(r["shade_ms"], 2),
                                                     "render": round(r["render_ms"], 2)} for r in timed_ranks]}
+        rms = [r["render_ms"] for r in timed_ranks if r["render_ms"] > 0]
+        if rms:
+            # balance of the tile partition: the slowest rank's render over the mean (device time of
+            # each rank's last render; rehearsed ranks on one device get equal chunk budgets)
+            group_info["rank_render_ms"] = {"max": round(max(rms), 2), "mean": round(float(np.mean(rms)), 2),
+                                            "max_over_mean": round(max(rms) / float(np.mean(rms)), 4)}
+        if len(set(group_devs)) > 1:
+            group_info["note"] = ("distinct-device group: ranks render concurrently, films reduced by RCCL; "
+                                  "film_reduce_bit_exact (--verify-film) is its check on this run")
         group_parallelism = ("tile-sharded x%d, one process (rtg_group: a handle and host thread per device) + "
                              "%s film reduce" % (len(group_devs), "RCCL ncclReduce" if rt.g.uses_rccl
                                                  else "host-memory (repeated devices)"))
@@ -446,7 +456,8 @@ def main():
                        if a.config == "C3" else "Mray/s (closest-hit + shadow rays), config %s" % a.config),
             "value": round(mrays, 2),
             "unit": "Mray/s",
-            "n_gpus": world if group_devs is None else len(group_devs),
+            "n_gpus": world if group_devs is None else len(set(group_devs)),
+            **({"ranks": len(group_devs)} if group_devs is not None else {}),
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_step, 3),
@@ -468,65 +479,71 @@ def main():
                        "parallelism": ("tile-sharded x%d + %s film reduce" % (world, "RCCL" if backend == "nccl" else backend)
                                        if group_devs is None else
                                        group_parallelism)},
-            "roofline": {"bound": "dependent-random-record-fetches", "kernel": "k_trace (extension + shadow rays)",
-                         "achieved": None if achieved_rec is None else round(achieved_rec, 1),
-                         "peak": (round(replay["ceiling_g_fetches_per_s"], 1) if replay else
-                                  None if ceiling is None else round(ceiling["g_lane_steps_per_s"], 1)),
-                         "unit": "G dependent random per-lane record fetches/s (node steps + triangle heads + leaf boxes)",
-                         "frac": (round(achieved_rec / replay["ceiling_g_fetches_per_s"], 4) if replay and achieved_rec else
-                                  round(achieved_rec / ceiling["g_lane_steps_per_s"], 4) if achieved_rec and ceiling else None),
-                         "peak_is": ("locality-matched in-repo ceiling (not a hardware peak): every launch's own fetch "
-                                     "stream of this workload captured and replayed on the scene's arrays with nothing "
-                                     "else in the loop (tools/roof_replay.py, %s)" % os.path.relpath(ROOF_REPLAY, ROOT)
-                                     if replay else
-                                     "in-repo microbenchmark ceiling (not a hardware peak): uniform random dependent "
-                                     "64-B records (tools/micro/roof.hip, %s)" % os.path.relpath(ROOF_SWEEP, ROOT)),
+            # headline roofline: a hardware peak. SURVEY.md 8d's algorithmic bytes of k_trace per
+            # launch / its average launch time, against the L2 aggregate bandwidth that serves them
+            # (they exceed the HBM peak: the ~70 MB hot scene lives in L2 + Infinity Cache, and the
+            # PMC-measured HBM bytes are `traffic`). The walk's limiter, dependent random record
+            # fetches, is priced in `fetches` against a microbenchmark and a replay of its own stream.
+            "roofline": {"bound": "l2", "kernel": "k_trace (extension + shadow rays)",
+                         "achieved": None if algo_gbs is None else round(algo_gbs, 1),
+                         "peak": L2_PEAK_GBS, "unit": "GB/s",
+                         "frac": None if algo_gbs is None else round(algo_gbs / L2_PEAK_GBS, 4),
+                         "frac_hw": None if algo_gbs is None else round(algo_gbs / L2_PEAK_GBS, 4),
+                         "peak_is": "MI355X aggregate L2 bandwidth, /opt/skills/guides/MI355X_MICROARCH.md (L2 per XCD)",
+                         "definition": ("SURVEY.md 8d: 32 B x box tests + 36 B x triangle tests + 48 B per ray, box / "
+                                        "triangle tests of the reference BVH2 walk counted on this workload; per launch "
+                                        "= bytes of the launch's rays / avg_launch_ms"),
+                         "bytes_per_ray": round(b_ray, 1), "bytes_per_shadow_ray": round(b_sray, 1),
+                         "box_tests_per_ray": round(boxes_per_ray, 2), "tri_tests_per_ray": round(tris_per_ray, 2),
+                         "shadow_box_tests_per_ray": round(s_boxes_per_ray, 2),
+                         "shadow_tri_tests_per_ray": round(s_tris_per_ray, 2),
+                         "frac_of_hbm_peak": None if algo_gbs is None else round(algo_gbs / HBM_PEAK_GBS, 4),
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                          "traffic": traffic,
                          "traffic_source": (None if traffic is None else
                                             "%s: rocprofv3 PMC (FETCH_SIZE x1 for the gathers + WRITE_SIZE, DRAM share) "
                                             "of this workload in separate passes; from profiles/, not measured in this run"
                                             % os.path.relpath(PMC_SUMMARY, ROOT)),
-                         "frac_uniform_random_ceiling": (round(achieved_rec / ceiling["g_lane_steps_per_s"], 4)
-                                                         if achieved_rec and ceiling else None),
-                         "uniform_random_ceiling": (None if ceiling is None else
-                                                    {"peak": round(ceiling["g_lane_steps_per_s"], 1),
-                                                     "source": "tools/micro/roof.hip, %s: dependent random 64-B per-lane "
-                                                               "records, %d MiB table, %d VALU/step"
-                                                               % (os.path.relpath(ROOF_SWEEP, ROOT), ceiling["table_mib"],
-                                                                  ceiling["valu_per_step"])}),
-                         "replay": (None if not replay else
-                                    {"k_trace_ms": round(replay["k_trace_ms"], 2), "replay_ms": round(replay["replay_ms"], 2),
-                                     "replayed_fetches": replay["replayed_fetches"],
-                                     "frac_at_measurement": round(replay["frac"], 4)}),
-                         "fetches_per_ray": round(rec_step / max(all_rays, 1), 2),
-                         "requests": {"achieved": None if achieved_req is None else round(achieved_req, 1),
-                                      "peak": None if ceiling is None else round(ceiling["g_req_per_s"], 1),
-                                      "unit": "G 16-B vector-memory requests/s",
-                                      "frac": (round(achieved_req / ceiling["g_req_per_s"], 4)
-                                               if achieved_req and ceiling else None),
-                                      "per_ray": round(req_step / max(all_rays, 1), 2)},
-                         "tri_tail_loads_per_ray": round(cw["tri_tail_loads"] / max(all_rays, 1), 2),
-                         "leafbox_tests_per_ray": round(cw["leafbox_tests"] / max(all_rays, 1), 2),
-                         "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                         "hw_peaks": {
-                             "hbm": {"bytes_per_launch": traffic,
-                                     "achieved_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic and extend_ms > 0 else None,
-                                     "peak_gbs": HBM_PEAK_GBS,
-                                     "frac": (round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4)
-                                              if traffic and extend_ms > 0 else None),
-                                     "source": "PMC (traffic_source)"},
-                             "l2_algorithmic": {"definition": "SURVEY.md 8d: 32 B x box tests + 36 B x triangle tests + "
-                                                              "48 B per ray, reference BVH2 walk counts",
-                                                "achieved_gbs": None if algo_gbs is None else round(algo_gbs, 1),
-                                                "served_by": "L1 / L2 / Infinity Cache (scene ~70 MB hot)",
-                                                "peak_gbs": L2_PEAK_GBS,
-                                                "frac": None if algo_gbs is None else round(algo_gbs / L2_PEAK_GBS, 4),
-                                                "frac_of_hbm_peak": None if algo_gbs is None else round(algo_gbs / HBM_PEAK_GBS, 4),
-                                                "bytes_per_ray": round(b_ray, 1), "box_tests_per_ray": round(boxes_per_ray, 2),
-                                                "tri_tests_per_ray": round(tris_per_ray, 2),
-                                                "bytes_per_shadow_ray": round(b_sray, 1),
-                                                "shadow_box_tests_per_ray": round(s_boxes_per_ray, 2),
-                                                "shadow_tri_tests_per_ray": round(s_tris_per_ray, 2)}},
+                         "hbm": {"bytes_per_launch": traffic,
+                                 "achieved_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic and extend_ms > 0 else None,
+                                 "peak_gbs": HBM_PEAK_GBS,
+                                 "frac": (round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4)
+                                          if traffic and extend_ms > 0 else None),
+                                 "source": "PMC (traffic_source)"},
+                         # the measured limiter: dependent random per-lane record fetches
+                         "fetches": {
+                             "achieved": None if achieved_rec is None else round(achieved_rec, 1),
+                             "unit": "G dependent random per-lane record fetches/s (node steps + triangle heads + leaf boxes)",
+                             "per_ray": round(rec_step / max(all_rays, 1), 2),
+                             "uniform_random_ceiling": (None if ceiling is None else
+                                                        {"peak": round(ceiling["g_lane_steps_per_s"], 1),
+                                                         "frac": (round(achieved_rec / ceiling["g_lane_steps_per_s"], 4)
+                                                                  if achieved_rec else None),
+                                                         "source": "tools/micro/roof.hip, %s: dependent random 64-B per-lane "
+                                                                   "records, %d MiB table, %d VALU/step (microbenchmark)"
+                                                                   % (os.path.relpath(ROOF_SWEEP, ROOT), ceiling["table_mib"],
+                                                                      ceiling["valu_per_step"])}),
+                             "replay_ceiling": (None if not replay else
+                                                {"peak": round(replay["ceiling_g_fetches_per_s"], 1),
+                                                 "frac_vs_replay": (round(achieved_rec / replay["ceiling_g_fetches_per_s"], 4)
+                                                                    if achieved_rec else None),
+                                                 "k_trace_ms": round(replay["k_trace_ms"], 2),
+                                                 "replay_ms": round(replay["replay_ms"], 2),
+                                                 "replayed_fetches": replay["replayed_fetches"],
+                                                 "frac_at_measurement": round(replay["frac"], 4),
+                                                 "source": ("this workload's own fetch stream captured and replayed with "
+                                                            "nothing else in the loop (tools/roof_replay.py); read from %s, "
+                                                            "a stored profile, not measured in this run; self-referential: "
+                                                            "it keeps the walk's fetch count and locality"
+                                                            % os.path.relpath(ROOF_REPLAY, ROOT))}),
+                             "requests": {"achieved": None if achieved_req is None else round(achieved_req, 1),
+                                          "peak": None if ceiling is None else round(ceiling["g_req_per_s"], 1),
+                                          "unit": "G 16-B vector-memory requests/s",
+                                          "frac": (round(achieved_req / ceiling["g_req_per_s"], 4)
+                                                   if achieved_req and ceiling else None),
+                                          "per_ray": round(req_step / max(all_rays, 1), 2)},
+                             "tri_tail_loads_per_ray": round(cw["tri_tail_loads"] / max(all_rays, 1), 2),
+                             "leafbox_tests_per_ray": round(cw["leafbox_tests"] / max(all_rays, 1), 2)},
                          "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from an own 3-axis SAH tree over the reference leaves)",
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
@@ -565,15 +582,19 @@ def main():
         dist.destroy_process_group()
 
 
-def dropin_leg(rt, a, tiles):
+def dropin_leg(rt, a, tiles, base_flags):
     """C3 through the drop-in frame loop: RTBase's Main.cpp calls RayTracer::render() once per frame
     (Main.cpp:74-118), and render() adds one sample per pixel (Renderer.h:876-885). Each frame here
     is one 1-spp librtg call, a.dropin_frames frames per repetition, under three host policies:
       queued      rtg_render_async(1 spp) per frame (what integration/rtg_rtbase.h's rtg_render_frame
-                  does), the film read back once at the end (saveHDR): frames overlap on the GPU
+                  does), the film read back once at the end (saveHDR): consecutive queued frames are
+                  coalesced (16 per chunk on a 1-Mpixel film) and chunks overlap on the GPU
+      queued_each the same with RTG_OPT_NO_COALESCE: every 1-spp call issued at once as its own chunk,
+                  up to three in flight on their own streams
       sync        rtg_render(1 spp) per frame (returns when the frame is on the film), one read at the end
       sync_read   rtg_render + rtg_film_read (12.6 MB D2H) every frame: round 3's rtg_render_frame
     The film of every policy is compared bit for bit with one batched render of the same samples."""
+    from raytracingrenderer_amd import _native as N
     F = a.dropin_frames
     out = {"frames_per_rep": F, "reps": a.dropin_reps, "spp_per_call": 1,
            "reference": "Main.cpp:74-118 frame loop, RayTracer::render() = 1 spp (Renderer.h:876-885)"}
@@ -582,6 +603,7 @@ def dropin_leg(rt, a, tiles):
     batch_film = rt.film()[0].view(np.uint32).copy()
 
     def run(policy):
+        rt.set_options(flags=base_flags | (N.RTG_OPT_NO_COALESCE if policy == "queued_each" else 0))
         best = None
         same = True
         rays = 0
@@ -590,7 +612,7 @@ def dropin_leg(rt, a, tiles):
             rt.synchronize()
             t0 = time.perf_counter()
             for f in range(F):
-                rt.render(1, tiles=tiles, first_sample=f, sync=(policy != "queued"))
+                rt.render(1, tiles=tiles, first_sample=f, sync=policy.startswith("sync"))
                 if policy == "sync_read":
                     rt.film()
             film = rt.film()[0]
@@ -601,8 +623,9 @@ def dropin_leg(rt, a, tiles):
             best = dt if best is None or dt < best else best
         return {"ms_per_frame": round(best * 1e3 / F, 4), "mrays_per_s": round(rays / best / 1e6, 1),
                 "film_equals_batched": same}
-    for pol in ("queued", "sync", "sync_read"):
+    for pol in ("queued", "queued_each", "sync", "sync_read"):
         out[pol] = run(pol)
+    rt.set_options(flags=base_flags)
     out["batched_ms_per_frame"] = None  # filled by the caller (ms_per_step / spp of the headline)
     return out
 

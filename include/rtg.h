@@ -148,6 +148,7 @@ void rtg_destroy(rtg_handle* h);
 #define RTG_OPT_WAVETIME 16  /* diagnostic builds only (RTG_DEBUG=1): per-wave clocks of k_trace on stderr */
 #define RTG_OPT_SERIAL  32   /* one chunk in flight at a time, every k_shade grid sized from the live counts
                                 read back during the traversal (verification / A-B of the frame pipeline) */
+#define RTG_OPT_NO_COALESCE 64  /* queued calls (rtg_render_async, no stream) are issued one by one */
 int  rtg_set_options(rtg_handle* h, int max_depth, int flags, uint32_t max_paths_in_flight);
 
 /* Per-pixel estimator (the alternative RayTracer methods of Renderer.h). PATH is RayTracer::render's
@@ -169,15 +170,19 @@ int  rtg_set_integrator(rtg_handle* h, int integrator);
  * sample order per pixel. Equivalent to n_samples calls of RayTracer::render() with the
  * deterministic sampler.
  * rtg_render returns when the samples are on the film. rtg_render_async only queues them:
- *   - with hip_stream NULL it is the drop-in RayTracer::render() of a frame loop (Main.cpp:74-118).
- *     A call of at most 8M paths (n_samples x pixels; a 1-spp frame up to 8 Mpixel) is queued
- *     without any host wait and returns before its work starts; consecutive calls run side by side
- *     on the GPU (up to 3 frames in flight, each with its own path state), their film updates still
- *     in sample order, so the film is bit-identical to one rtg_render of all the samples. Larger calls
- *     read each bounce's live count back during the traversal and return once their last launch is
- *     queued. Anything that reads the film or the stats (rtg_film_read with a film pointer,
- *     rtg_film_copy_device, rtg_get_stats, rtg_synchronize, rtg_clear ...) first waits for the
- *     queued frames; rtg_film_read(h, NULL, &spp) returns Film::SPP at once.
+ *   - with hip_stream NULL it is the drop-in RayTracer::render() of a frame loop (Main.cpp:74-118):
+ *     the call is queued and returns before its work starts. Consecutive queued calls with the same
+ *     seed and tiles whose samples follow on (frame f, f+1, ...) are coalesced and issued together
+ *     once 16M paths are pending (16 frames of a 1-Mpixel film), or as soon as anything reads the
+ *     film or the stats, waits, or changes a setting (RTG_OPT_NO_COALESCE issues every call at
+ *     once). Issued work of at most 8M paths per chunk runs in a pipeline of 3 slots, each with its
+ *     own path state and stream, with no host wait: chunks run side by side on the GPU, a call waits
+ *     only for the chunk three before it to leave the GPU, and the film updates stay in sample
+ *     order, so the film is bit-identical to one rtg_render of all the samples. Larger chunks read
+ *     each bounce's live count back during the traversal. rtg_film_read with a film pointer,
+ *     rtg_film_copy_device, rtg_get_stats, rtg_synchronize, rtg_render_idle, rtg_clear ... first
+ *     issue and wait for the queued calls; rtg_film_read(h, NULL, &spp) returns Film::SPP at once.
+ *     An error of a coalesced call is reported by the call that issues it.
  *   - with a hip_stream, the work is ordered after the caller's earlier work on that stream, and
  *     the caller's later work on it sees the film updated.
  * rtg_render_idle sets *idle to 1 when no queued render work is left on the GPU.

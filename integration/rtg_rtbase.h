@@ -2,14 +2,17 @@
 // reference to render on the MI355X (INTEGRATION.md §2 shows this file; it is the compiled code).
 //
 // Include it after RTBase's own headers (Scene.h pulls in Geometry.h, Materials.h, Lights.h,
-// Imaging.h) with include/ on the include path and link -lrtg. Two functions:
+// Imaging.h) with include/ on the include path and link -lrtg. Three functions:
 //
 //   rtg_flatten_scene(scene, binding)   RTBase's built Scene (Scene.h:72-106, after Scene::build:
 //                                       triangles in post-sort order, Scene::lights in reference
 //                                       order) -> rtg_scene_desc, a copy: the vectors it points
 //                                       into live in the binding
 //   rtg_render_frame(gpu, film, seed)   RayTracer::render() (Renderer.h:876-885): film->SPP++, one
-//                                       sample of every pixel on the GPU, Film::film read back
+//                                       sample of every pixel queued on the GPU (up to three frames
+//                                       run side by side; the call returns at once)
+//   rtg_film_sync(gpu, film)            Film::film brought up to date (waits for the queued frames):
+//                                       before saveHDR / savePNG / presentFilmToCanvas
 //
 // RayTracer::init (Renderer.h:45-63) then creates the handle once:
 //     rtg_flatten_scene(scene, binding);
@@ -138,11 +141,15 @@ inline void rtg_flatten_scene(Scene* s, RtgSceneBinding& b) {
     d.projection.a_film = c.Afilm;
 }
 
-// RayTracer::render() (Renderer.h:876-885): one frame = one sample of every pixel, all tiles.
+// RayTracer::render() (Renderer.h:876-885): one frame = one sample of every pixel, all tiles,
+// queued (rtg_render_async): Main.cpp's loop (Main.cpp:74-118) reads the film only to save it.
 inline int rtg_render_frame(rtg_handle* gpu, Film* film, uint64_t seed) {
     film->incrementSPP();
-    int rc = rtg_render(gpu, (uint32_t)film->SPP - 1, 1, seed, nullptr, 0);
-    if (rc) return rc;
+    return rtg_render_async(gpu, (uint32_t)film->SPP - 1, 1, seed, nullptr, 0, nullptr);
+}
+
+// Film::film of every frame queued so far (the read-back waits for them; 12 B per pixel).
+inline int rtg_film_sync(rtg_handle* gpu, Film* film) {
     uint32_t spp = 0;
     return rtg_film_read(gpu, (float*)film->film, &spp);
 }

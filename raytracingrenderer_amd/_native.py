@@ -11,6 +11,7 @@ LIB_DIR = os.path.join(_HERE, "lib")
 
 RTG_MAT_DIFFUSE, RTG_MAT_LAMBERT, RTG_MAT_MIRROR, RTG_MAT_GLASS = 0, 1, 2, 3
 RTG_OPT_CULL, RTG_OPT_COUNT, RTG_OPT_TIMING, RTG_OPT_BVH2, RTG_OPT_WAVETIME, RTG_OPT_SERIAL = 1, 2, 4, 8, 16, 32
+RTG_OPT_NO_COALESCE = 64
 RTG_INTEGRATOR_PATH, RTG_INTEGRATOR_DIRECT, RTG_INTEGRATOR_ALBEDO, RTG_INTEGRATOR_NORMALS = 0, 1, 2, 3
 RTG_INTEGRATOR_DIRECT_MIS = 4
 

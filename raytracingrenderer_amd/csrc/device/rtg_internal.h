@@ -205,6 +205,9 @@ static int dev_upload(T** dst, const std::vector<T>& src) {
 #ifndef RTG_PIPE_MAX_P
 #define RTG_PIPE_MAX_P (8u << 20)
 #endif
+#ifndef RTG_COALESCE_P
+#define RTG_COALESCE_P (16u << 20)         // queued frames are issued once this many paths are pending
+#endif
 #ifndef RTG_HOSTGRID_MIN_TILES
 #define RTG_HOSTGRID_MIN_TILES 4096u       // big chunks: seg_tiles at or above this size the k_shade grid
 #endif                                     // from the read-back counts
@@ -216,6 +219,7 @@ struct ChunkSlot {
     size_t cap_ovf = 0;
     hipStream_t stream = nullptr;
     hipEvent_t fold = nullptr;  // this slot's last film fold (k_accumulate) has run
+    bool used = false;          // fold has been recorded
 };
 
 struct rtg_handle {
@@ -225,6 +229,8 @@ struct rtg_handle {
     uint32_t spp = 0;
     int max_depth = 4, cull = 1, count = 0, timing = 0, serial = 0;
     uint32_t max_paths = 1u << 30;  // 1G paths in flight at most; the chunk is held to half the free HBM
+    size_t mem_cap = 0;  // != 0: path-state budget of this handle (a group rehearsing k ranks on one
+                         // device gives each 1/k of half the device's free HBM, so their chunks match)
     int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0;
     int wavetime = 0;  // RTG_DEBUG builds: per-wave clocks of the first chunk (RTG_OPT_WAVETIME)
     int capture_launch = -1;  // RTG_DEBUG builds: trace launch of chunk 0 whose fetches are captured
@@ -258,6 +264,13 @@ struct rtg_handle {
     hipEvent_t entry = nullptr;    // recorded on the caller's stream when a render starts: chunks wait on it
     hipEvent_t last_fold = nullptr;  // the last queued chunk's fold (a slot's event; null before any)
     bool inflight = false;         // chunks queued by rtg_render_async(.., NULL) not yet joined to `stream`
+    // queued calls not yet issued (rtg_render_async with no stream): consecutive calls of the same
+    // seed and tiles whose samples follow on are coalesced into one chunk of up to RTG_COALESCE_P
+    // paths, issued when that fills or when anything reads, waits or changes a setting
+    uint32_t pend_first = 0, pend_n = 0;
+    uint64_t pend_seed = 0;
+    std::vector<uint32_t> pend_key;
+    int no_coalesce = 0;           // RTG_OPT_NO_COALESCE: every queued call is issued at once
     unsigned* d_pix = nullptr;
     size_t cap_pix = 0;
     std::vector<uint32_t> pix_key;
@@ -310,7 +323,9 @@ int ensure_chunk(rtg_handle* h, ChunkSlot& sl, size_t P, int maxb, bool queues);
 // lazy: chunks stay queued past the return (rtg_render_async with no stream); join_frames later makes
 // the handle's stream wait for them. Otherwise `st` waits for them before render_impl returns.
 int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed, const uint32_t* tiles,
-                uint32_t n_tiles, hipStream_t st, bool lazy);
+                uint32_t n_tiles, hipStream_t st, bool lazy, bool add_spp = true);
+// issue the coalesced queued calls (rtg_render_async with no stream) not issued yet
+int flush_pending(rtg_handle* h);
 // the handle's stream waits for every queued chunk (called by every entry point that reads the film,
 // the stats or slot 0's buffers, or synchronises)
 int join_frames(rtg_handle* h);

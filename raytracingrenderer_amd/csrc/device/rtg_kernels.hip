@@ -1042,20 +1042,30 @@ __global__ void k_probe_math(int fn, const float* in, int n, float* out) {
     }
 }
 
-// Per-chunk ray tally: extension + shadow queue lengths of every bounce into stats[2..3].
+// Per-chunk ray tally: extension + shadow queue lengths of every bounce into stats[2..3]. One wave:
+// lane j reads the counters of (bounce, segment) pairs j, j + 64, ... (a lone thread's dependent
+// walk over 9 x maxb counters took ~80 us, on the critical path of a 1-spp frame)
 __global__ void k_tally(const Counters* ctr, int maxb, unsigned long long* stats) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int lane = threadIdx.x;
     unsigned long long e = 0, sh = 0;
-    for (int b = 0; b < maxb; ++b) {
-        e += ctr[b].n_ext;
-        sh += ctr[b].n_shadow;
-        for (int k = 0; k < 8; ++k) {  // segmented queues (path tracer)
+    for (int j = lane; j < maxb * 9; j += 64) {
+        const int b = j / 9, k = j % 9;
+        if (k == 8) {
+            e += ctr[b].n_ext;
+            sh += ctr[b].n_shadow;
+        } else {  // segmented queues (path tracer)
             e += ctr[b].ne8[32 * k];
             sh += ctr[b].ns8[32 * k];
         }
     }
-    atomicAdd(&stats[2], e);  // chunk pipelines may tally concurrently
-    atomicAdd(&stats[3], sh);
+    for (int off = 32; off > 0; off >>= 1) {
+        e += __shfl_down(e, off);
+        sh += __shfl_down(sh, off);
+    }
+    if (lane == 0) {
+        atomicAdd(&stats[2], e);  // chunks in flight tally concurrently
+        atomicAdd(&stats[3], sh);
+    }
 }
 
 // ================================================================== host side (C-ABI)
@@ -1078,16 +1088,33 @@ static void free_chunk(ChunkSlot& sl) {
 static size_t path_bytes(int planes, bool queues) { return (size_t)200 + (size_t)16 * (size_t)planes + (queues ? 8u : 0u); }
 static size_t slot_bytes(const ChunkSlot& sl) { return sl.cap_P * path_bytes(sl.cap_maxb, sl.pb.q[0] != nullptr); }
 
-static int ensure_stream(ChunkSlot& sl) {
-    if (!sl.stream) HIPOK(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+#ifndef RTG_SLOT_STREAMS
+#define RTG_SLOT_STREAMS 2  // 0: plain streams, 1: one priority per slot, 2: full-CU-mask streams
+#endif
+static int ensure_stream(rtg_handle* h, ChunkSlot& sl) {
+    if (!sl.stream) {
+        const int k = (int)(&sl - h->slot);
+        if (RTG_SLOT_STREAMS == 2) {
+            // a stream with a CU mask gets an HSA queue of its own: plain streams beyond
+            // GPU_MAX_HW_QUEUES share queues, and two slots on one queue run in turn
+            std::vector<uint32_t> mask((h->n_cu + 31) / 32, 0xffffffffu);
+            if (h->n_cu % 32) mask.back() = (1u << (h->n_cu % 32)) - 1u;
+            HIPOK(hipExtStreamCreateWithCUMask(&sl.stream, (uint32_t)mask.size(), mask.data()));
+        } else if (RTG_SLOT_STREAMS == 1) {
+            int lo = 0, hi = 0;
+            HIPOK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPOK(hipStreamCreateWithPriority(&sl.stream, hipStreamNonBlocking, k == 0 ? lo : k == 1 ? hi : (lo + hi) / 2));
+        } else {
+            HIPOK(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+        }
+    }
     if (!sl.fold) HIPOK(hipEventCreateWithFlags(&sl.fold, hipEventDisableTiming));
     return RTG_OK;
 }
 
 int ensure_chunk(rtg_handle* h, ChunkSlot& sl, size_t P, int maxb, bool queues) {
-    (void)h;
     int rc;
-    if ((rc = ensure_stream(sl))) return rc;
+    if ((rc = ensure_stream(h, sl))) return rc;
     PathBufs& p = sl.pb;
     if (P <= sl.cap_P && maxb <= sl.cap_maxb) {
         if (queues && !p.q[0]) {
@@ -1140,7 +1167,18 @@ int ensure_ovf(rtg_handle* h, ChunkSlot& sl) {
     return RTG_OK;
 }
 
+int flush_pending(rtg_handle* h) {
+    if (!h->pend_n) return RTG_OK;
+    const uint32_t first = h->pend_first, n = h->pend_n;
+    h->pend_n = 0;
+    const bool all = h->pend_key.size() == 1 && h->pend_key[0] == 0xffffffffu;
+    const std::vector<uint32_t> key = h->pend_key;
+    return render_impl(h, first, n, h->pend_seed, all ? nullptr : key.data(), all ? 0u : (uint32_t)key.size(),
+                       h->stream, true, false);
+}
+
 int join_frames(rtg_handle* h) {
+    if (int rc = flush_pending(h)) return rc;
     if (!h->inflight) return RTG_OK;
     h->inflight = false;
     HIPOK(hipStreamWaitEvent(h->stream, h->last_fold, 0));
@@ -1699,6 +1737,7 @@ int rtg_create(int device, const rtg_scene_desc* desc, rtg_handle** out) {
 void rtg_destroy(rtg_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    h->pend_n = 0;  // queued calls not issued yet are dropped with the film
     if (h->stream) {
         (void)join_frames(h);
         (void)hipStreamSynchronize(h->stream);
@@ -1729,12 +1768,14 @@ int rtg_set_integrator(rtg_handle* h, int integrator) {
         g_err = "rtg_set_integrator: bad argument";
         return RTG_ERR_ARG;
     }
+    if (int rc = flush_pending(h)) return rc;  // queued calls render with the settings they were queued under
     h->integrator = integrator;
     return RTG_OK;
 }
 
 int rtg_set_options(rtg_handle* h, int max_depth, int cull, uint32_t max_paths) {
     if (!h || max_depth < 0 || max_depth > 250) { g_err = "rtg_set_options: bad argument"; return RTG_ERR_ARG; }
+    if (int rc = flush_pending(h)) return rc;  // queued calls render with the settings they were queued under
     h->max_depth = max_depth;
     h->cull = cull & 1;
     h->count = (cull >> 1) & 1;   // bit 1: counting kernels (node/triangle tests)
@@ -1742,6 +1783,7 @@ int rtg_set_options(rtg_handle* h, int max_depth, int cull, uint32_t max_paths) 
     h->wide = ((cull >> 3) & 1) ? 0 : 1;  // bit 3: force the reference BVH2 walk
     h->wavetime = RTG_DEBUG ? (cull >> 4) & 1 : 0;  // bit 4 (RTG_DEBUG builds): per-wave clocks
     h->serial = (cull >> 5) & 1;  // bit 5: no frame pipeline, read-back k_shade grids
+    h->no_coalesce = (cull >> 6) & 1;  // bit 6: queued calls are issued one by one
     if (max_paths) h->max_paths = max_paths;
     return RTG_OK;
 }
@@ -1835,7 +1877,7 @@ static void print_wavetime(const std::vector<unsigned long long>& wt, int maxb, 
 }
 
 int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed,
-                       const uint32_t* tiles, uint32_t n_tiles, hipStream_t st, bool lazy) {
+                       const uint32_t* tiles, uint32_t n_tiles, hipStream_t st, bool lazy, bool add_spp) {
     int rc = set_pixels(h, tiles, n_tiles);
     if (rc) return rc;
     if (h->npix == 0 || n_samples == 0) return RTG_OK;
@@ -1853,7 +1895,8 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
             size_t held = 0;
             for (const ChunkSlot& sl : h->slot) held += slot_bytes(sl);
-            const size_t budget = (freeb + held) / 2;
+            size_t budget = (freeb + held) / 2;
+            if (h->mem_cap) budget = std::min(budget, h->mem_cap);
             const size_t per_pix = path_bytes(planes, false) * std::max<size_t>(1, h->npix);
             size_t max_ns = budget / per_pix;
             if (!diag && (size_t)ns_chunk * h->npix <= RTG_PIPE_MAX_P) max_ns = budget / RTG_SLOTS / per_pix;
@@ -1907,6 +1950,9 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     uint32_t c = 0;
     for (uint32_t s0 = first; s0 < first + n_samples; s0 += ns_chunk, ++c) {
         ChunkSlot& sl = pipe ? h->slot[h->next_slot++ % RTG_SLOTS] : h->slot[0];
+        // back-pressure: a slot takes its next chunk once its previous one has left the GPU, so at
+        // most RTG_SLOTS chunks are in flight and the host stays at most that far ahead
+        if (pipe && sl.used) HIPOK(hipEventSynchronize(sl.fold));
         if ((rc = ensure_chunk(h, sl, P, planes, false))) return rc;
         if ((rc = ensure_ovf(h, sl))) return rc;
         const hipStream_t ss = sl.stream;
@@ -2036,6 +2082,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         LAUNCH_OK("k_accumulate");
         timed_end(h, ss, k); kinds.push_back(2); ++k;
         HIPOK(hipEventRecord(sl.fold, ss));
+        sl.used = true;
         h->last_fold = sl.fold;
         h->inflight = true;
         h->stats.paths += a.P;
@@ -2048,7 +2095,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             print_wavetime(wt, maxb, wt_waves);
         }
     }
-    h->spp += n_samples;
+    if (add_spp) h->spp += n_samples;
     if (lazy) return RTG_OK;
     // the caller's stream waits for the chunks (and for every chunk queued before them)
     h->inflight = false;
@@ -2078,13 +2125,35 @@ int rtg_render_async(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, c
                      uint32_t n_tiles, void* stream) {
     if (!h) { g_err = "null handle"; return RTG_ERR_ARG; }
     HIPOK(hipSetDevice(h->device));
-    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
-    return render_impl(h, first, n, seed, tiles, n_tiles, st, stream == nullptr);
+    if (stream) {
+        if (int rc = flush_pending(h)) return rc;
+        return render_impl(h, first, n, seed, tiles, n_tiles, (hipStream_t)stream, false);
+    }
+    if (n == 0) return RTG_OK;
+    if ((uint64_t)first + n > 65536u) { g_err = "sample index >= 65536 (PCG stream key)"; return RTG_ERR_ARG; }
+    // queued: coalesced with the pending calls when it continues them (same seed and tiles, the
+    // next sample indices); otherwise those are issued first
+    std::vector<uint32_t> key;
+    if (tiles) key.assign(tiles, tiles + n_tiles);
+    else key.push_back(0xffffffffu);
+    if (h->pend_n && (key != h->pend_key || seed != h->pend_seed || first != h->pend_first + h->pend_n))
+        if (int rc = flush_pending(h)) return rc;
+    if (int rc = set_pixels(h, tiles, n_tiles)) return rc;  // (validates the tiles; a no-op when unchanged)
+    if (!h->pend_n) {
+        h->pend_first = first;
+        h->pend_seed = seed;
+        h->pend_key.swap(key);
+    }
+    h->pend_n += n;
+    h->spp += n;  // Film::SPP counts the queued frames at once
+    if (h->no_coalesce || (uint64_t)h->pend_n * h->npix >= RTG_COALESCE_P) return flush_pending(h);
+    return RTG_OK;
 }
 
 int rtg_render(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, const uint32_t* tiles, uint32_t n_tiles) {
     if (!h) { g_err = "null handle"; return RTG_ERR_ARG; }
     HIPOK(hipSetDevice(h->device));
+    if (int rc = flush_pending(h)) return rc;
     int rc = render_impl(h, first, n, seed, tiles, n_tiles, h->stream, false);
     if (rc) return rc;
     return rtg_synchronize(h);
@@ -2093,6 +2162,7 @@ int rtg_render(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, const u
 int rtg_render_idle(rtg_handle* h, int* idle) {
     if (!h || !idle) { g_err = "rtg_render_idle: null argument"; return RTG_ERR_ARG; }
     HIPOK(hipSetDevice(h->device));
+    if (int rc = flush_pending(h)) return rc;  // queued calls not issued yet are work left
     *idle = 1;
     if (h->last_fold) {
         const hipError_t e = hipEventQuery(h->last_fold);
@@ -2314,6 +2384,7 @@ int rtg_film_load(rtg_handle* h, const float* rgb, uint32_t spp) {
 int rtg_clear(rtg_handle* h) {
     if (!h) return RTG_ERR_ARG;
     HIPOK(hipSetDevice(h->device));
+    h->pend_n = 0;  // queued calls not issued yet: the clear would zero what they add
     if (int rc = join_frames(h)) return rc;
     HIPOK(hipMemsetAsync(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float), h->stream));
     HIPOK(hipMemsetAsync(h->d_stats, 0, 16 * sizeof(unsigned long long), h->stream));

@@ -10,9 +10,9 @@
 // bit-identical to a one-GPU render, whatever the reduction order.
 //
 // A device list that repeats a device (rehearsing N ranks on one GPU) cannot form an RCCL
-// communicator; the ranks then render one after another (concurrent handles on one GPU would each
-// size their path state from the same free-memory reading) and the films are summed through host
-// memory in rank order (same bits).
+// communicator; the ranks then render one after another, each with an equal share of the device's
+// memory for its chunks (rtg_handle::mem_cap), and the films are summed through host memory in
+// rank order (same bits).
 //
 // Setup: the scene's device records are built once on the host (prepare_scene: triangle records,
 // the wide tree over the reference leaves, leaf boxes, materials, textures) and uploaded to every
@@ -178,6 +178,17 @@ int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* de
     std::vector<int> sorted(g->devices);
     std::sort(sorted.begin(), sorted.end());
     g->distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (!g->distinct) {
+        // ranks rehearsed on one device render in turn, each keeping its chunk buffers: give each
+        // an equal share of half the device's free HBM, so every rank runs the same chunk sizes
+        // (left to the free-memory reading, later ranks got ever smaller chunks)
+        for (int r = 0; r < n_devices; ++r) {
+            const int k = (int)std::count(g->devices.begin(), g->devices.end(), g->devices[r]);
+            size_t freeb = 0, totalb = 0;
+            if (hipSetDevice(g->devices[r]) == hipSuccess && hipMemGetInfo(&freeb, &totalb) == hipSuccess)
+                g->h[r]->mem_cap = std::max<size_t>(1, freeb / 2 / (size_t)k);
+        }
+    }
     if (g->distinct) {
         if (!load_rccl()) {
             rtg_group_destroy(g);

@@ -7,9 +7,13 @@
 // 'P' and 'L' (saveHDR / savePNG of -outputFilename) become: -outputFilename is always written at
 // the end, as .hdr or, for a .png name, tonemapped PNG (RayTracer::savePNG).
 // Extra options (defaults keep the reference behaviour): -width -height (override scene.json),
-// -maxDepth (MAX_DEPTH, 4), -seed (sampler seed, 1234), -device, -batch (spp per rtg_render call;
-// results do not depend on it), -skipMissing 1 (filtered scene variants), -envmap <file>,
-// -timeLimit <s> (10; 0 = none).
+// -maxDepth (MAX_DEPTH, 4), -seed (sampler seed, 1234), -device, -batch (spp per render call;
+// results do not depend on it), -sync 1 (wait for every frame; default: frames are queued with
+// rtg_render_async and up to three run side by side, the film is read once at the end),
+// -skipMissing 1 (filtered scene variants), -envmap <file>, -timeLimit <s> (10; 0 = none).
+// "Frame time" is the wall time of each render call, as Main.cpp:113-117 times rt.render(); with
+// queued frames a call returns once the frame three before it has left the GPU, so in the steady
+// state it is the GPU's time per frame.
 // Multi-GPU (one node): -gpus N renders on devices 0..N-1, -devices a,b,... on a list. Rank r
 // renders the 32x32 tiles with (tile_x + tile_y) % N == r, one host thread per device, and the films
 // are summed into the first device by one RCCL reduce before the film is written (rtg_group_*,
@@ -58,6 +62,7 @@ int main(int argc, char** argv) {
     const int device = std::stoi(get("-device", "0"));
     const unsigned batch = (unsigned)std::max(1, std::stoi(get("-batch", "1")));
     const double time_limit = std::stod(get("-timeLimit", "10"));
+    const bool sync = std::stoi(get("-sync", "0")) != 0;
 
     rth_scene* scene = nullptr;
     if (rth_load_scene(scene_name.c_str(), &lo, &scene) != 0) return die("loadScene", rth_last_error());
@@ -88,10 +93,13 @@ int main(int argc, char** argv) {
 
     unsigned spp = 0;
     double total = 0.0;
+    const auto w0 = std::chrono::steady_clock::now();
     while (spp < spp_target) {
         const unsigned n = std::min(batch, spp_target - spp);
         auto t0 = std::chrono::steady_clock::now();
-        const int rc = grp ? rtg_group_render(grp, spp, n, seed) : rtg_render(rt, spp, n, seed, nullptr, 0);
+        const int rc = grp    ? rtg_group_render(grp, spp, n, seed)
+                       : sync ? rtg_render(rt, spp, n, seed, nullptr, 0)
+                              : rtg_render_async(rt, spp, n, seed, nullptr, 0, nullptr);
         if (rc != 0) return die("rtg_render", rtg_last_error());
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         total += dt;
@@ -101,6 +109,11 @@ int main(int argc, char** argv) {
     }
     std::vector<float> film((size_t)info.width * info.height * 3);
     uint32_t got = 0;
+    if (rt && rtg_synchronize(rt) != 0) return die("rtg_synchronize", rtg_last_error());
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
+    std::printf("%u spp in %.4f s of wall time (%s): %.4f ms per spp, %.1f Mpaths/s\n", spp, wall,
+                grp ? "device group" : sync ? "synchronous calls" : "queued calls", 1e3 * wall / std::max(1u, spp),
+                (double)spp * info.width * info.height / wall / 1e6);
     if (grp) {
         if (rtg_group_film_read(grp, film.data(), &got) != 0) return die("rtg_group_film_read", rtg_last_error());
         std::printf("film reduce: %.3f ms\n", rtg_group_reduce_ms(grp));

@@ -27,6 +27,12 @@ def test_bench_line_contract():
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in rf, k
     assert 0.3 < rf["frac"] <= 1.05 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 0.01
+    assert rf["peak"] == 34500.0 and rf["unit"] == "GB/s"  # a hardware peak (MI355X aggregate L2)
+    # the drop-in frame loop: 1-spp calls, films bit-identical to the batched render
+    di = d["dropin"]
+    for pol in ("queued", "sync", "sync_read"):
+        assert di[pol]["film_equals_batched"] is True and di[pol]["ms_per_frame"] > 0, pol
+    assert di["queued"]["ms_per_frame"] <= di["sync_read"]["ms_per_frame"]
     cb = d["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cb, k

@@ -190,16 +190,20 @@ def test_queue_segment_edges(w, h, spp, max_paths, serial):
     assert_bitexact(film, ref, "%dx%d x%d spp, max_paths %d" % (w, h, spp, max_paths))
 
 
-def test_queued_frames_return_early_and_equal_one_render(tmp_path):
+@pytest.mark.parametrize("coalesce", [True, False])
+def test_queued_frames_return_early_and_equal_one_render(tmp_path, coalesce):
     """The drop-in frame loop (Main.cpp:74-118: one RayTracer::render() per frame): 1-spp
-    rtg_render_async calls are queued with no host wait and return before their work has run; up to
-    three frames run side by side, and the film, folded in sample order, is bit-identical to one
-    rtg_render of all the samples. Film::SPP is readable at once; a film read waits for the frames."""
+    rtg_render_async calls are queued and return before their work has run; consecutive ones are
+    coalesced into one chunk (or, with RTG_OPT_NO_COALESCE, each issued at once, up to three chunks
+    running side by side), and the film, folded in sample order, is bit-identical to one rtg_render
+    of all the samples. Film::SPP is readable at once; a film read waits for the frames."""
     d = str(tmp_path / "s")
     write_synthetic_scene(d, n_tris=200000, seed=5, width=1024, height=1024)
     s = loadScene(d)
     full = gpu_film(s, 12, seed=99)
     rt = RayTracer(s, seed=99)
+    if not coalesce:
+        rt.set_options(flags=rt.flags | N.RTG_OPT_NO_COALESCE)
     rt.render(1, sync=False)  # warm: buffers of the first slots
     rt.clear()
     rt.synchronize()
@@ -207,7 +211,8 @@ def test_queued_frames_return_early_and_equal_one_render(tmp_path):
     for f in range(12):
         rt.render(1, first_sample=f, sync=False)
         if f == 0:
-            # a 1M-path frame of a 200k-triangle scene runs for milliseconds; the call returned at once
+            # a 1M-path frame of a 200k-triangle scene runs for milliseconds; the call returned at
+            # once (rtg_render_idle issues a coalesced frame before it looks)
             assert not rt.idle(), "rtg_render_async waited for its frame"
     assert rt.getSPP() == 12
     film, spp = rt.film()
