@@ -175,7 +175,7 @@ int  rtg_set_integrator(rtg_handle* h, int integrator);
  *     seed and tiles whose samples follow on (frame f, f+1, ...) are coalesced and issued together
  *     once 16M paths are pending (16 frames of a 1-Mpixel film), or as soon as anything reads the
  *     film or the stats, waits, or changes a setting (RTG_OPT_NO_COALESCE issues every call at
- *     once). Issued work of at most 8M paths per chunk runs in a pipeline of 3 slots, each with its
+ *     once). Issued work of at most 16M paths per chunk runs in a pipeline of 3 slots, each with its
  *     own path state and stream, with no host wait: chunks run side by side on the GPU, a call waits
  *     only for the chunk three before it to leave the GPU, and the film updates stay in sample
  *     order, so the film is bit-identical to one rtg_render of all the samples. Larger chunks read

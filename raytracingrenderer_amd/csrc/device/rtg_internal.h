@@ -191,8 +191,8 @@ static int dev_upload(T** dst, const std::vector<T>& src) {
     return RTG_OK;
 }
 
-// Chunks in flight (the frame pipeline). A chunk of at most RTG_PIPE_MAX_P paths -- one 1-spp frame
-// of a film up to 8 Mpixel, the drop-in RayTracer::render() -- is issued without any host wait (its
+// Chunks in flight (the frame pipeline). A chunk of at most RTG_PIPE_MAX_P paths -- the coalesced
+// 1-spp frames of the drop-in RayTracer::render() (RTG_COALESCE_P) -- is issued without any host wait (its
 // k_shade grids cover every tile a segment can hold; blocks past the live count exit at once) into the
 // next of RTG_SLOTS slots, each with its own path state, stack overflow and stream, so consecutive
 // frames run side by side on the GPU and fill each other's drain tails. The film folds stay in sample
@@ -203,7 +203,7 @@ static int dev_upload(T** dst, const std::vector<T>& src) {
 #define RTG_SLOTS 3                        // with the handle's stream, 4 = GPU_MAX_HW_QUEUES streams
 #endif
 #ifndef RTG_PIPE_MAX_P
-#define RTG_PIPE_MAX_P (8u << 20)
+#define RTG_PIPE_MAX_P (16u << 20)
 #endif
 #ifndef RTG_COALESCE_P
 #define RTG_COALESCE_P (16u << 20)         // queued frames are issued once this many paths are pending
