@@ -121,7 +121,7 @@ struct __align__(16) DevMat {
 struct __align__(16) DevLight {
     float4 v0a;  // v0.xyz, area       (area light)
     float4 v1t;  // v1.xyz, type bits  (0 area, 1 environment)
-    float4 v2;   // v2.xyz
+    float4 v2;   // v2.xyz, 1.0f / area (Triangle::sample's pdf, divided on the host)
     float4 gn;   // gNormal.xyz        (Triangle::gNormal)
     float4 em;   // emission rgb
 };
@@ -143,7 +143,9 @@ struct SceneView {
     const DevLight* lights;
     const DevTex* texinfo;
     const float4* texels;  // RGB + pad per texel
+    int n_mats;          // distinct material records (prepare_scene merges identical ones)
     int n_lights;
+    float pmf;           // 1.f / (float)n_lights, Scene::sampleLight's pmf, divided on the host
     int env_tex;         // -1: BackgroundColour(0)
     int env_off, env_w, env_h;  // the environment texture (first texel, size), kernel-argument copies
     int root_word;       // child word of the root (RTG_EXIT if no triangles)
@@ -199,6 +201,17 @@ RTG_D v3 tex_sample(const SceneView& s, const DevMat& M, float tu, float tv) {
                     M.tex_wh == 0x10001 ? &M.texel0 : nullptr);
 }
 
+// ------------------------------------------------------------------ division by a constant
+// The reference divides by M_PI in float (Colour / M_PI, Materials.h:131, 140) and in binary64
+// (wi.z / M_PI, Sampling.h:52-56; u / (2 * M_PI) and acosf(wi.y) / M_PI, Lights.h:152-153). A
+// binary64 product with the reciprocal, rounded to float, gives the same bits for every one of the
+// 2^32 float inputs (oracle/div_rewrites.c, checked in tests/test_math.py): a few cycles instead of
+// a correctly rounded division sequence (v_div_scale / rcp / fma / div_fmas / div_fixup).
+RTG_D float div_pi_f(float x) { return (float)((double)x * (1.0 / (double)RTG_PI_F)); }  // x / (float)M_PI
+RTG_D float div_pi_d(float x) { return (float)((double)x * (1.0 / RTM_PI)); }            // (float)((double)x / M_PI)
+RTG_D float div_2pi_d(float x) { return (float)((double)x * (1.0 / (2.0 * RTM_PI))); }   // (float)((double)x / (2 M_PI))
+RTG_D v3 divs_pi(v3 a) { return mk(div_pi_f(a.x), div_pi_f(a.y), div_pi_f(a.z)); }       // divs(a, (float)M_PI)
+
 // ------------------------------------------------------------------ sampling (Sampling.h)
 RTG_D v3 spherical_to_world(float theta, float phi) {  // Core.h:547-550
     float st, ct, sp, cp;  // rtm_sincosf: bit-identical to rtm_sinf / rtm_cosf
@@ -222,8 +235,8 @@ RTG_D float uniform_sphere_pdf() { return (float)(1.0 / (4.0 * RTM_PI)); }
 RTG_D v3 env_eval(const SceneView& s, v3 wi) {
     float u = rtm_atan2f(wi.z, wi.x);
     u = (u < 0.0f) ? (float)((double)u + 2.0 * RTM_PI) : u;
-    u = (float)((double)u / (2.0 * RTM_PI));
-    float v = (float)((double)rtm_acosf(wi.y) / RTM_PI);
+    u = div_2pi_d(u);                // (float)((double)u / (2.0 * M_PI))
+    float v = div_pi_d(rtm_acosf(wi.y));  // (float)((double)acosf(wi.y) / M_PI)
     return bilinear(Texels4{s.texels + s.env_off}, s.env_w, s.env_h, u, v);
 }
 RTG_D v3 background(const SceneView& s, v3 dir) {
@@ -292,9 +305,9 @@ RTG_D v3 bsdf_sample(int kind, float int_ior, float ext_ior, v3 alb, const frame
         const float q2 = smp.next();
         const float q1 = smp.next();
         const v3 wl = cosine_sample_hemisphere(q1, q2);
-        if (kind == 0) pdf = (wl.z >= 0.0f) ? (float)((double)wl.z / RTM_PI) : 0.0f;  // cosineHemispherePDF
-        else pdf = (float)((double)wl.z / RTM_PI);                                      // stubs: wi.z / M_PI
-        refl = divs(alb, RTG_PI_F);
+        if (kind == 0) pdf = (wl.z >= 0.0f) ? div_pi_d(wl.z) : 0.0f;  // cosineHemispherePDF
+        else pdf = div_pi_d(wl.z);                                      // stubs: wi.z / M_PI
+        refl = divs_pi(alb);
         return to_world(fr, wl);
     }
     const v3 wol = to_local(fr, wo);
@@ -329,7 +342,7 @@ RTG_D v3 bsdf_sample(int kind, float int_ior, float ext_ior, v3 alb, const frame
 // (Materials.h:136-140, 227-232, 349-354, 394-399, 447-452; Sampling.h:52-56). Only z of toLocal is used.
 RTG_D float bsdf_pdf_lambert(const frame& fr, v3 wi) {
     const float z = dot(wi, fr.w);
-    return (z >= 0.0f) ? (float)((double)z / RTM_PI) : 0.0f;
+    return (z >= 0.0f) ? div_pi_d(z) : 0.0f;
 }
 // RayTracer::convertPDFAreaToSolidAngle / balanceHeuristic (Renderer.h:411-422)
 RTG_D float pdf_area_to_solid(float pdf_area, float dist2, float cos_theta) {

@@ -46,6 +46,12 @@ using namespace rtgd;
 #ifndef RTG_TAIL_BATCH
 #define RTG_TAIL_BATCH 64
 #endif
+#ifndef RTG_LDS_MATS
+#define RTG_LDS_MATS 64     // k_shade holds the material table in LDS up to this many records (64 B each)
+#endif
+#ifndef RTG_LDS_LIGHTS
+#define RTG_LDS_LIGHTS 48   // ... and the light table up to this many (80 B each): 5 x 48 < 256 threads
+#endif
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 7   // min waves per SIMD for k_shade (72 VGPRs, no spills; one tile per block)
 #endif
@@ -128,7 +134,25 @@ struct ChunkArgs {
                                // PCG seed, canHitLight); k_generate writes ray_d only
     unsigned seg_tiles = 0;    // tiles of 256 per queue segment (Counters::ne8); k_shade grid = 8x
     // path ids are pixel-major: pid = lp * ns + sl (a wave of camera rays is one pixel's samples)
+    unsigned long long ns_mul = 0;  // lp = (pid * ns_mul) >> ns_shift (set_ns_div); 0: divide
+    unsigned ns_shift = 0;
 };
+// pid / ns as a multiply. With 2^l >= ns, S = 31 + l and M = ceil(2^S / ns) < 2^32, the excess
+// e = M ns - 2^S < ns <= 2^l. Writing pid = q ns + r, pid M / 2^S = q + r / ns + pid e / (ns 2^S),
+// and the last two terms stay below 1 when pid e < 2^S, i.e. for every pid < 2^31: the floor is q.
+static inline void set_ns_div(ChunkArgs& a) {
+    a.ns_mul = 0;
+    if ((unsigned long long)a.P > (1ull << 31)) return;
+    unsigned l = 0;
+    while ((1u << l) < a.ns) ++l;
+    const unsigned S = 31 + l;
+    a.ns_mul = ((1ull << S) + a.ns - 1) / a.ns;
+    a.ns_shift = S;
+}
+static __device__ __forceinline__ void split_pid(const ChunkArgs& a, unsigned pid, unsigned& lp, unsigned& sl) {
+    lp = a.ns_mul ? (unsigned)(((unsigned long long)pid * a.ns_mul) >> a.ns_shift) : pid / a.ns;
+    sl = pid - lp * a.ns;
+}
 
 struct PathBufs {
     // extension payload, two sets (the path tracer's bounce b reads set b & 1 by queue position and

@@ -568,7 +568,8 @@ __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
     }
     if (!a.seg_tiles && pid == 0) p.ctr[0].n_ext = a.P;  // instant radiosity's camera pass: one queue
     if (pid >= a.P) return;
-    const unsigned lp = pid / a.ns, sl = pid % a.ns;  // pixel-major path ids
+    unsigned lp, sl;  // pixel-major path ids
+    split_pid(a, pid, lp, sl);
     const unsigned pixel = a.pixlist[lp];
     const unsigned W = (unsigned)a.cam.width;
     const unsigned x = pixel % W, y = pixel / W;
@@ -607,11 +608,17 @@ __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
 // path id for k_accumulate.
 // ALT = false: pathTrace only (RayTracer::render's estimator; the other modes compile away).
 // ALT = true: every per-pixel estimator of rtg_set_integrator, selected by a.mode.
-template <bool ALT>
+// TAB = true: the scene's material and light records (at most RTG_LDS_MATS / RTG_LDS_LIGHTS) are
+// copied into LDS while the payload and the hit triangle's shading record load, so the material a
+// shading record names is an LDS read, not a dependent global fetch: the chain per path is payload ->
+// shading record -> (texels of a texture larger than 1x1).
+template <bool ALT, bool TAB>
 __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
     __shared__ unsigned s_cnt[2][RTG_TB / 64];
     __shared__ unsigned s_base[2];
     __shared__ float4 s_sho[RTG_TB], s_shd[RTG_TB];  // NEE ray staged until its queue position is known
+    __shared__ DevMat s_mat[TAB ? RTG_LDS_MATS : 1];
+    __shared__ DevLight s_lt[TAB ? RTG_LDS_LIGHTS : 1];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     const bool lean0 = b == 0;  // bounce 0: path id = position, camera origin, thr 1, PCG seed, canHitLight
@@ -635,6 +642,19 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
     float4* out_t = (b & 1) ? p.thr : p.thr2;
     unsigned long long* out_r = (b & 1) ? p.rng : p.rng2;
     float4* contrib = p.contrib + (size_t)b * a.P;
+    // material / light tables: global -> LDS directly (global_load_lds_dwordx4, no VGPRs), 16 B per
+    // thread; a wave's lanes fill 64 consecutive pieces from the wave's base
+    if (TAB) {
+        typedef __attribute__((address_space(1))) const void* gptr_t;
+        typedef __attribute__((address_space(3))) void* lptr_t;
+        const unsigned w0 = threadIdx.x & ~63u;
+        if ((int)threadIdx.x < 4 * s.n_mats)
+            __builtin_amdgcn_global_load_lds((gptr_t)(reinterpret_cast<const float4*>(s.mats) + threadIdx.x),
+                                             (lptr_t)(reinterpret_cast<float4*>(s_mat) + w0), 16, 0, 0);
+        if ((int)threadIdx.x < 5 * s.n_lights)
+            __builtin_amdgcn_global_load_lds((gptr_t)(reinterpret_cast<const float4*>(s.lights) + threadIdx.x),
+                                             (lptr_t)(reinterpret_cast<float4*>(s_lt) + w0), 16, 0, 0);
+    }
     // one 256-path tile per block: a finished block frees its slot for the next tile
     {
         const unsigned i = base + threadIdx.x;
@@ -645,16 +665,24 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
         float4 n_o = make_float4(0.0f, 0.0f, 0.0f, 0.0f), n_d = n_o, n_t = n_o;
         unsigned long long n_r = 0;
         const bool valid = i < n;
+        // the payload and, on a hit, the triangle's shading record (issued before the tables' barrier)
+        float4 ro = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f), rd = ro, h = ro;
+        DevShade S;
         if (valid) {
-            const float4 ro = lean0 ? make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f) : in_o[i];
+            if (!lean0) ro = in_o[i];
+            rd = in_d[i];
+            h = p.hits[i];
+            if (h.x < RTG_FLT_MAX) S = s.shade[__float_as_int(h.y)];
+        }
+        if (TAB) __syncthreads();  // (waits for the table loads: vmcnt(0))
+        if (valid) {
             pid = lean0 ? (int)i : __float_as_int(ro.w);  // the path id travels in ray_o.w
-            const float4 rd = in_d[i];
-            const float4 h = p.hits[i];
             const v3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
             const float4 thr4 = lean0 ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : in_t[i];
             v3 thr = mk(thr4.x, thr4.y, thr4.z);
             const int can_hit = lean0 ? 1 : (rd.w != 0.0f);  // canHitLight travels in ray_d.w
-            const unsigned lp = (unsigned)pid / a.ns, sl = (unsigned)pid % a.ns;
+            unsigned lp, sl;
+            split_pid(a, (unsigned)pid, lp, sl);
             const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);  // (carrying it in the payload: slower)
             uint64_t st = lean0 ? pcg_seed(a.seed, inc) : in_r[i];
             v3 c;
@@ -670,9 +698,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                 if (B.y != 0.0f && c0.w == 1.0f) {
                     nterms = 1;
                 } else if (h.x < RTG_FLT_MAX) {
-                    const int tri = __float_as_int(h.y);
-                    const DevShade S = s.shade[tri];
-                    const DevMat M = s.mats[__float_as_int(S.d.w)];
+                    const DevMat& M = TAB ? s_mat[__float_as_int(S.d.w)] : s.mats[__float_as_int(S.d.w)];
                     if (M.is_light) {
                         const float alpha = h.z, beta = h.w, gamma = 1.0f - (alpha + beta);
                         const v3 x2 = add(o, muls(d, h.x));
@@ -694,12 +720,10 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                 c = (!ALT || a.mode == RTG_INTEGRATOR_PATH || a.mode == RTG_INTEGRATOR_ALBEDO) ? background(s, d)
                                                                                              : mk(0.0f, 0.0f, 0.0f);
             } else {
-                const int tri = __float_as_int(h.y);
                 const float alpha = h.z, beta = h.w, gamma = 1.0f - (alpha + beta);
                 const float t = h.x;
                 const v3 x = add(o, muls(d, t));  // Ray::at
-                const DevShade S = s.shade[tri];
-                const DevMat& M = s.mats[__float_as_int(S.d.w)];
+                const DevMat& M = TAB ? s_mat[__float_as_int(S.d.w)] : s.mats[__float_as_int(S.d.w)];
                 const v3 n0 = mk(S.a.x, S.a.y, S.a.z), n1 = mk(S.a.w, S.b.x, S.b.y), n2 = mk(S.b.z, S.b.w, S.c.x);
                 v3 sn = normalize(add(add(muls(n0, alpha), muls(n1, beta)), muls(n2, gamma)));
                 const float tu = (S.c.y * alpha + S.c.w * beta) + S.d.y * gamma;
@@ -714,18 +738,18 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                         : can_hit ? mul(thr, mk(M.emission.x, M.emission.y, M.emission.z)) : mk(0.0f, 0.0f, 0.0f);
                 } else if (ALT && a.mode == RTG_INTEGRATOR_ALBEDO) {  // BSDF::evaluate(sd, (0,1,0))
                     const v3 alb = tex_sample(s, M, tu, tv);
-                    c = M.kind == RTG_MAT_MIRROR ? alb : (M.kind == RTG_MAT_GLASS ? mk(0.0f, 0.0f, 0.0f) : divs(alb, RTG_PI_F));
+                    c = M.kind == RTG_MAT_MIRROR ? alb : (M.kind == RTG_MAT_GLASS ? mk(0.0f, 0.0f, 0.0f) : divs_pi(alb));
                 } else if (ALT && a.mode == RTG_INTEGRATOR_DIRECT_MIS) {
                     // computeDirectMIS, first half (Renderer.h:474-519): one light sample weighted by
                     // the balance heuristic (its shadow ray), then one BSDF sample (its extension ray)
                     c = mk(0.0f, 0.0f, 0.0f);
                     if (!(M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS)) {
                         const int nl = s.n_lights;
-                        const float pmf = 1.f / (float)nl;
+                        const float pmf = s.pmf;  // 1.f / (float)nl
                         int li = (int)((float)nl * pcg_next(st, inc));
                         li = (nl - 1) < li ? (nl - 1) : li;
-                        const DevLight L = s.lights[li];
-                        const v3 f = divs(tex_sample(s, M, tu, tv), RTG_PI_F);  // BSDF::evaluate
+                        const DevLight L = TAB ? s_lt[li] : s.lights[li];
+                        const v3 f = divs_pi(tex_sample(s, M, tu, tv));  // BSDF::evaluate
                         float pdf;
                         float env_flag = 0.0f;
                         if (__float_as_int(L.v1t.w) == 0) {
@@ -734,7 +758,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                             const float la = 1 - sqrtf(r1);
                             const float lb = r2 * sqrtf(r1);
                             const float lg = 1.0f - (la + lb);
-                            pdf = 1.0f / L.v0a.w;
+                            pdf = L.v2.w;  // 1.0f / area
                             const v3 p2 = add(add(muls(mk(L.v0a.x, L.v0a.y, L.v0a.z), la), muls(mk(L.v1t.x, L.v1t.y, L.v1t.z), lb)),
                                               muls(mk(L.v2.x, L.v2.y, L.v2.z), lg));
                             v3 wi = sub(p2, x);
@@ -805,10 +829,10 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                     v3 cpre = ld;
                     if (!spec) {
                         const int nl = s.n_lights;
-                        const float pmf = 1.f / (float)nl;
+                        const float pmf = s.pmf;  // 1.f / (float)nl
                         int li = (int)((float)nl * pcg_next(st, inc));
                         li = (nl - 1) < li ? (nl - 1) : li;  // (std::min)(a, b)
-                        const DevLight L = s.lights[li];
+                        const DevLight L = TAB ? s_lt[li] : s.lights[li];
                         v3 p2, wi;
                         float g, pdf;
                         v3 emitted;
@@ -818,7 +842,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                             const float la = 1 - sqrtf(r1);
                             const float lb = r2 * sqrtf(r1);
                             const float lg = 1.0f - (la + lb);
-                            pdf = 1.0f / L.v0a.w;
+                            pdf = L.v2.w;  // 1.0f / area
                             p2 = add(add(muls(mk(L.v0a.x, L.v0a.y, L.v0a.z), la), muls(mk(L.v1t.x, L.v1t.y, L.v1t.z), lb)),
                                      muls(mk(L.v2.x, L.v2.y, L.v2.z), lg));
                             emitted = mk(L.em.x, L.em.y, L.em.z);
@@ -841,7 +865,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                             const float maxt = sqrtf(length_sq(sd)) - (2.0f * RTG_EPS);
                             sd = normalize(sd);
                             const v3 so = add(x, muls(sd, RTG_EPS));
-                            const v3 f = divs(alb, RTG_PI_F);  // BSDF::evaluate
+                            const v3 f = divs_pi(alb);  // BSDF::evaluate
                             ld = divs(muls(mul(f, emitted), g), pmf * pdf);
                             const v3 cvis = mul(thr, ld);
                             s_sho[threadIdx.x] = make_float4(so.x, so.y, so.z, maxt);
@@ -1019,7 +1043,7 @@ __global__ void k_probe_bsdf(const float* in, int n, float* out) {
     v3 refl;
     float pdf;
     const v3 wi = bsdf_sample(kind, c[1], c[2], alb, fr, wo, smp, refl, pdf);
-    const v3 ev = kind <= 1 ? divs(alb, RTG_PI_F) : (kind == 2 ? alb : mk(0.0f, 0.0f, 0.0f));
+    const v3 ev = kind <= 1 ? divs_pi(alb) : (kind == 2 ? alb : mk(0.0f, 0.0f, 0.0f));
     float* o = out + (size_t)i * 11;
     o[0] = wi.x; o[1] = wi.y; o[2] = wi.z;
     o[3] = refl.x; o[4] = refl.y; o[5] = refl.z;
@@ -1599,6 +1623,21 @@ int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
         mats[i].pad = 0;
         mats[i].texel0 = make_float4(texels[(size_t)t.off * 4], texels[(size_t)t.off * 4 + 1], texels[(size_t)t.off * 4 + 2], 0.0f);
     }
+    // Identical material records merged (a scene file gives every instance its own BSDF: bathroom_f
+    // has 852 for 24 distinct ones), so k_shade can hold the table in LDS; the triangles' shading
+    // records are remapped. Same record, same arithmetic: the output does not change.
+    {
+        std::vector<DevMat> uniq;
+        std::vector<int> remap(mats.size());
+        for (size_t i = 0; i < mats.size(); ++i) {
+            size_t j = 0;
+            while (j < uniq.size() && std::memcmp(&uniq[j], &mats[i], sizeof(DevMat)) != 0) ++j;
+            if (j == uniq.size()) uniq.push_back(mats[i]);
+            remap[i] = (int)j;
+        }
+        for (uint32_t i = 0; i < nt; ++i) shade[i].d.w = host_bits_f(remap[d->material[i]]);
+        mats.swap(uniq);
+    }
     std::vector<DevLight> lights(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; ++i) {
         int li = d->lights[i];
@@ -1614,7 +1653,7 @@ int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
         const float* em = d->materials[d->material[li]].emission;
         L.v0a = make_float4(P[0], P[1], P[2], tri_area[li]);
         L.v1t = make_float4(P[3], P[4], P[5], host_bits_f(0));
-        L.v2 = make_float4(P[6], P[7], P[8], 0.0f);
+        L.v2 = make_float4(P[6], P[7], P[8], 1.0f / tri_area[li]);  // Triangle::sample's pdf
         L.gn = make_float4(tri_gn[li * 3], tri_gn[li * 3 + 1], tri_gn[li * 3 + 2], 0.0f);
         L.em = make_float4(em[0], em[1], em[2], 0.0f);
     }
@@ -1685,7 +1724,9 @@ int upload_scene(int device, const HostScene& hs, rtg_handle* h) {
     s.lights = h->d_lights;
     s.texinfo = h->d_texinfo;
     s.texels = (const float4*)h->d_texels;
+    s.n_mats = (int)hs.mats.size();
     s.n_lights = hs.n_lights;
+    s.pmf = 1.f / (float)hs.n_lights;  // Scene::sampleLight (Scene.h:137-138), the same IEEE division
     s.env_tex = hs.env_tex;
     s.env_off = hs.env_off;
     s.env_w = hs.env_w;
@@ -1975,6 +2016,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         a.cam = h->cam;
         a.lean = 1;
         a.seg_tiles = (unsigned)seg_tiles(a.P);
+        set_ns_div(a);
         // k_shade grids from the live counts read back while the traversal runs (big chunks), or over
         // every tile a segment can hold (blocks past the live count exit at once): no host wait
         const bool hostgrid = !pipe && (a.seg_tiles >= RTG_HOSTGRID_MIN_TILES || h->serial);
@@ -2004,10 +2046,11 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                 }
                 if (tiles) {
                     timed_begin(h, ss, k);
-                    if (h->integrator == RTG_INTEGRATOR_PATH)
-                        hipLaunchKernelGGL(k_shade<false>, dim3(8 * tiles), dim3(RTG_TB), 0, ss, h->sv, a, pb, b - 1);
-                    else
-                        hipLaunchKernelGGL(k_shade<true>, dim3(8 * tiles), dim3(RTG_TB), 0, ss, h->sv, a, pb, b - 1);
+                    const bool tab = h->sv.n_mats <= RTG_LDS_MATS && h->sv.n_lights <= RTG_LDS_LIGHTS;
+                    const bool alt = h->integrator != RTG_INTEGRATOR_PATH;
+                    auto kern = alt ? (tab ? k_shade<true, true> : k_shade<true, false>)
+                                    : (tab ? k_shade<false, true> : k_shade<false, false>);
+                    hipLaunchKernelGGL(kern, dim3(8 * tiles), dim3(RTG_TB), 0, ss, h->sv, a, pb, b - 1);
                     LAUNCH_OK("k_shade");
                     timed_end(h, ss, k); kinds.push_back(2); ++k;
                 }

@@ -152,7 +152,7 @@ __global__ __launch_bounds__(RTG_TB) void k_light_generate(SceneView s, LightArg
         uint64_t st = pcg_seed(a.seed, inc);
         // Scene::sampleLight (Scene.h:131-140)
         const int nl = s.n_lights;
-        const float pmf = 1.f / (float)nl;
+        const float pmf = s.pmf;  // 1.f / (float)nl
         int li = (int)((float)nl * pcg_next(st, inc));
         li = (nl - 1) < li ? (nl - 1) : li;
         const DevLight L = s.lights[li];
@@ -163,14 +163,14 @@ __global__ __launch_bounds__(RTG_TB) void k_light_generate(SceneView s, LightArg
             const float la = 1 - sqrtf(r1);
             const float lb = r2 * sqrtf(r1);
             const float lg = 1.0f - (la + lb);
-            const float pdf_pos = 1.0f / L.v0a.w;
+            const float pdf_pos = L.v2.w;  // 1.0f / area
             const v3 pt = add(add(muls(mk(L.v0a.x, L.v0a.y, L.v0a.z), la), muls(mk(L.v1t.x, L.v1t.y, L.v1t.z), lb)),
                               muls(mk(L.v2.x, L.v2.y, L.v2.z), lg));
             // sampleDirectionFromLight (Lights.h:67-80): cosineSampleHemisphere(next(), next()), first draw -> r2
             const float q2 = pcg_next(st, inc);
             const float q1 = pcg_next(st, inc);
             const v3 wl = cosine_sample_hemisphere(q1, q2);
-            const float pdf_dir = (wl.z >= 0.0f) ? (float)((double)wl.z / RTM_PI) : 0.0f;
+            const float pdf_dir = (wl.z >= 0.0f) ? div_pi_d(wl.z) : 0.0f;
             const v3 gn = mk(L.gn.x, L.gn.y, L.gn.z);
             const frame fr = frame_from(gn);
             const v3 wi = to_world(fr, wl);
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(RTG_TB) void k_light_shade(SceneView s, LightArgs a
                 if (M.is_light || spec) {
                     cont = false;  // lightTracePath returns at lights and pure specular surfaces
                 } else {
-                    const v3 f = divs(tex_sample(s, M, tu, tv), RTG_PI_F);  // BSDF::evaluate
+                    const v3 f = divs_pi(tex_sample(s, M, tu, tv));  // BSDF::evaluate
                     const v3 col = mul(mul(thr, f), le);
                     int pixel;
                     v3 cc;
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(RTG_TB) void k_light_shade(SceneView s, LightArgs a
                 }
             } else if (!M.is_light && !spec) {
                 // store a VPL: Le = pathThroughput * Le * evaluate(sd, -r.dir) * |(-r.dir) . sN|
-                const v3 f = divs(tex_sample(s, M, tu, tv), RTG_PI_F);
+                const v3 f = divs_pi(tex_sample(s, M, tu, tv));
                 const v3 vle = muls(mul(mul(thr, le), f), fabsf(dot(wo, sn)));
                 const unsigned r = atomicAdd(rec_n, 1u);
                 rec_key[r] = ((unsigned long long)i << 16) | k;
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(RTG_TB) void k_ir_first_hit(SceneView s, ChunkArgs 
         if (M.two_sided && dot(neg(d), sn) < 0) sn = neg(sn);
         const bool spec = M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS;
         flag = (M.is_light || spec) ? 1.0f : 2.0f;
-        if (!M.is_light && !spec) f = divs(tex_sample(s, M, tu, tv), RTG_PI_F);
+        if (!M.is_light && !spec) f = divs_pi(tex_sample(s, M, tu, tv));
     }
     px[lp] = make_float4(x.x, x.y, x.z, flag);
     pn[lp] = make_float4(sn.x, sn.y, sn.z, 0.0f);

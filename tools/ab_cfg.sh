@@ -1,0 +1,19 @@
+#!/bin/bash
+# A/B of the lib variants in raytracingrenderer_amd/lib/ab over several configs, 2 interleaved rounds:
+# C3 (headline), C2, C4 at 64 spp, C5 at 32 spp. Prints value and kernel ms per step.
+R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out; cd $R
+CFGS=${CFGS:-"C3 C2 C4 C5"}
+for round in 1 2; do
+for cfg in $CFGS; do
+for lib in raytracingrenderer_amd/lib/ab/*.so; do
+  case $cfg in
+    C3) args="--config C3 --steps 10 --warmup 2";;
+    C2) args="--config C2 --steps 20 --warmup 2";;
+    C4) args="--config C4 --spp 64 --steps 2 --warmup 1";;
+    C5) args="--config C5 --spp 32 --steps 2 --warmup 1";;
+  esac
+  RTG_LIB=$R/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --dropin-frames 0 $args > gpurun_out/ab.log 2> gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 1; }
+  echo "$cfg $(basename $lib) $(tail -1 gpurun_out/ab.log | python3 -c "
+import json,sys
+d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['kernel_ms_per_step_rank0'])")"
+done; done; done
