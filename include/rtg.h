@@ -136,8 +136,8 @@ void rtg_destroy(rtg_handle* h);
  * most max_depth+2 closest-hit segments. flags: RTG_OPT_CULL enables the conservative distance
  * culling (without it traversal visits exactly the reference's node set: verification mode);
  * RTG_OPT_COUNT runs the counting kernels (node / triangle tests in rtg_stats);
- * RTG_OPT_TIMING records HIP events around every launch (per-kernel-class ms in rtg_stats; implies
- * RTG_OPT_SERIAL);
+ * RTG_OPT_TIMING records HIP events around every launch (per-kernel-class ms in rtg_stats; launches
+ * of chunks running side by side in the frame pipeline each count their shared time);
  * RTG_OPT_BVH2 forces the reference BVH2 walk (no 4-wide collapse; verification / A-B).
  * max_paths_in_flight bounds the paths of one wavefront chunk (0 = keep, default 1G; a chunk's path
  * state is also held to half the free HBM). */

@@ -1927,8 +1927,9 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     // computeDirectMIS keeps two scratch planes of per-path state in contrib planes 2 and 3
     const int planes = h->integrator == RTG_INTEGRATOR_DIRECT_MIS ? std::max(maxb, 4) : maxb;
     uint32_t ns_chunk = std::max<uint32_t>(1, std::min<uint32_t>(n_samples, h->max_paths / std::max(1u, h->npix)));
-    // the diagnostic modes read one chunk's launches in order on one stream
-    const bool diag = h->timing || h->serial || (RTG_DEBUG && (h->wavetime || h->capture_launch >= 0));
+    // the diagnostic modes read one chunk's launches in order on one stream (per-launch timing
+    // events work across the slots' streams: overlapped launches then count their shared time twice)
+    const bool diag = h->serial || (RTG_DEBUG && (h->wavetime || h->capture_launch >= 0));
     {
         // path state of the chunks in flight takes at most half the free HBM (buffers held now count
         // as free); pipelined chunks keep RTG_SLOTS sets
@@ -1940,7 +1941,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             if (h->mem_cap) budget = std::min(budget, h->mem_cap);
             const size_t per_pix = path_bytes(planes, false) * std::max<size_t>(1, h->npix);
             size_t max_ns = budget / per_pix;
-            if (!diag && (size_t)ns_chunk * h->npix <= RTG_PIPE_MAX_P) max_ns = budget / RTG_SLOTS / per_pix;
+            if (lazy && !diag && (size_t)ns_chunk * h->npix <= RTG_PIPE_MAX_P) max_ns = budget / RTG_SLOTS / per_pix;
             ns_chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(ns_chunk, max_ns));
         }
     }
@@ -1959,9 +1960,12 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         ns_chunk = (n_samples + nchunks - 1) / nchunks;
     }
     const size_t P = (size_t)ns_chunk * h->npix;
-    // the frame pipeline (rtg_internal.h, ChunkSlot): small chunks rotate through the slots with no
-    // host wait; big ones run in slot 0 with the read-back k_shade grid
-    const bool pipe = !diag && P <= RTG_PIPE_MAX_P;
+    // the frame pipeline (rtg_internal.h, ChunkSlot): queued chunks of up to RTG_PIPE_MAX_P paths
+    // rotate through the slots with no host wait, so the next queued frames run beside them. A call
+    // that is waited for runs its chunks one at a time in slot 0: chunks of one render side by side
+    // measured slower than one chunk (C3 at N = 1 and rank 0's share of 8: the traversals slow each
+    // other down and add launches)
+    const bool pipe = lazy && !diag && P <= RTG_PIPE_MAX_P;
     (void)hipGetLastError();  // drop any stale error left by other code on this thread
     if (!h->inflight) HIPOK(hipEventRecord(h->ev[0], st));  // start of this render (or of a queued run)
     HIPOK(hipEventRecord(h->entry, st));  // every chunk starts after the caller's earlier work on st
