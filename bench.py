@@ -34,6 +34,12 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")  # rocprofv
 KSTATS = os.path.join(ROOT, "profiles", "r03_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
 ROOF_REPLAY = os.path.join(ROOT, "profiles", "r03_roof_replay.jsonl")  # tools/roof_replay.py (C3)
+# the replay ceiling of each workload (tools/roof_replay.py on an MI355X), by (config, shard_of)
+ROOF_REPLAYS = {("C3", 1): ROOF_REPLAY,
+                ("C3", 8): os.path.join(ROOT, "profiles", "r03_roof_replay_shard8.jsonl"),
+                ("C2", 1): os.path.join(ROOT, "profiles", "r03_roof_replay_c2.jsonl"),
+                ("C4", 1): os.path.join(ROOT, "profiles", "r03_roof_replay_c4_64spp.jsonl"),
+                ("C5", 1): os.path.join(ROOT, "profiles", "r04_roof_replay_c5_4spp.jsonl")}
 # k_shade's algorithmic bytes (PATH integrator; the payload travels with the queues):
 # every shaded path reads its direction 16, hit record 16, pixel 4 and, on a hit, the triangle's
 # shading record 64, and writes contrib 16 and meta 4; a path past the camera bounce also reads its
@@ -426,9 +432,11 @@ def main():
         except Exception:
             pmc = None
     replay = None
-    if profiled and os.path.exists(ROOF_REPLAY):
+    # (a rank of N renders rank 0's share of an N-way split up to the diagonal offset: shard-of N's ceiling)
+    replay_file = ROOF_REPLAYS.get((a.config, max(a.shard_of, world, 1))) if group_devs is None else None
+    if replay_file and os.path.exists(replay_file):
         try:
-            replay = [json.loads(l) for l in open(ROOF_REPLAY) if '"total"' in l][-1]
+            replay = [json.loads(l) for l in open(replay_file) if '"total"' in l][-1]
         except Exception:
             replay = None
     # k_shade: algorithmic payload bytes per step (SHADE_B_*) / its kernel time (the timed region's
@@ -535,7 +543,7 @@ def main():
                                                             "nothing else in the loop (tools/roof_replay.py); read from %s, "
                                                             "a stored profile, not measured in this run; self-referential: "
                                                             "it keeps the walk's fetch count and locality"
-                                                            % os.path.relpath(ROOF_REPLAY, ROOT))}),
+                                                            % os.path.relpath(replay_file, ROOT))}),
                              "requests": {"achieved": None if achieved_req is None else round(achieved_req, 1),
                                           "peak": None if ceiling is None else round(ceiling["g_req_per_s"], 1),
                                           "unit": "G 16-B vector-memory requests/s",
