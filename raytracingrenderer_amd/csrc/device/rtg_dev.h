@@ -153,6 +153,11 @@ struct SceneView {
     int usew;            // wide tree available (finite bounds, children inside parents)
     float root_box[6];   // bounds of the reference root node
     float cull_scale;    // scene magnitude used for the conservative cull inflation
+    // small scenes (the wide nodes, triangle records and leaf boxes fit RTG_SMALL_F4 float4s, e.g.
+    // the cornell box of config C2): one image [wide nodes | triangles | leaf boxes] that k_trace
+    // copies into LDS per block, so every record fetch of the walk is an LDS read
+    const float4* img;   // null: the walk reads global memory
+    int img_n4, img_tri, img_lb;  // image size and the float4 offsets of the triangles / leaf boxes
 };
 
 // ------------------------------------------------------------------ Texture::sample

@@ -25,6 +25,12 @@ using namespace rtgd;
 #define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (96 B per lane)
 #endif
 // (the tuning constants are overridable with -D for A/B builds: tools/ab_matrix.sh)
+#ifndef RTG_STACK_SMALL
+#define RTG_STACK_SMALL 11  // the LDS stack of k_trace's small-scene variant (with its scene image in LDS)
+#endif
+#ifndef RTG_SMALL_F4
+#define RTG_SMALL_F4 224    // small-scene image limit, float4s (3.5 KB): 11 x 256 B of stack + 3.5 KB per
+#endif                      // one-wave block keeps 24 blocks per CU in the 160 KB of LDS
 #ifndef RTG_POSTPONE
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
@@ -255,7 +261,7 @@ struct rtg_handle {
     uint32_t max_paths = 1u << 30;  // 1G paths in flight at most; the chunk is held to half the free HBM
     size_t mem_cap = 0;  // != 0: path-state budget of this handle (a group rehearsing k ranks on one
                          // device gives each 1/k of half the device's free HBM, so their chunks match)
-    int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0;
+    int n_cu = 256, trace_blocks = 0, trace_blocks_count = 0, trace_blocks_small = 0, trace_blocks_small_count = 0;
     int wavetime = 0;  // RTG_DEBUG builds: per-wave clocks of the first chunk (RTG_OPT_WAVETIME)
     int capture_launch = -1;  // RTG_DEBUG builds: trace launch of chunk 0 whose fetches are captured
     uint4* d_cap = nullptr;           // its chains (TraceIO::cap)
@@ -270,6 +276,7 @@ struct rtg_handle {
     DevNode* d_nodes = nullptr;
     DevNodeQ* d_nodesq = nullptr;
     float4* d_leafbox = nullptr;
+    float4* d_img = nullptr;   // the small-scene image (SceneView::img)
     int usew = 0, wide = 1;
     int integrator = RTG_INTEGRATOR_PATH;
     bool rebuilt = false;     // wide tree cut from rebuild_over_leaves (else from the reference BVH2)
@@ -321,6 +328,8 @@ struct HostScene {
     std::vector<DevNode> nodes;
     std::vector<DevNodeQ> nodesq;
     std::vector<float4> leafbox;
+    std::vector<float4> img;   // small scenes: [wide nodes | triangles | leaf boxes] (SceneView::img)
+    int img_tri = 0, img_lb = 0;
     std::vector<DevTri48> tris48;
     std::vector<DevShade> shade;
     std::vector<DevMat> mats;

@@ -27,6 +27,8 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -56,11 +58,16 @@ static __device__ __forceinline__ void trace_slice(const TraceIO& io, unsigned n
     }
 }
 
-template <bool COUNT>
+// SMALL: the scene's wide nodes, triangle records and leaf boxes are copied into LDS at the start of
+// each block (SceneView::img, small scenes only) and the walk reads them there; the LDS stack is then
+// RTG_STACK_SMALL entries, so the block's LDS stays what a 24-entry stack takes.
+template <bool COUNT, bool SMALL>
 __global__ __launch_bounds__(RTG_TTB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
 void k_trace(SceneView s, TraceIO io) {
-    __shared__ int stk[RTG_STACK][RTG_TTB];
-    __shared__ float kstk[COUNT ? RTG_STACK : 1][RTG_TTB];  // COUNT only: entry key of each push
+    constexpr int STK = SMALL ? RTG_STACK_SMALL : RTG_STACK;
+    __shared__ int stk[STK][RTG_TTB];
+    __shared__ float kstk[COUNT ? STK : 1][RTG_TTB];  // COUNT only: entry key of each push
+    __shared__ float4 s_img[SMALL ? RTG_SMALL_F4 : 1];
     const int tid = threadIdx.x;
     const int lane = lane_id();
     const unsigned gthreads = gridDim.x * blockDim.x;
@@ -83,7 +90,11 @@ void k_trace(SceneView s, TraceIO io) {
         s_tab[1][tid] = elen;
         s_tab[2][tid] = len;
     }
+    if (SMALL)
+        for (int i = tid; i < s.img_n4; i += RTG_TTB) s_img[i] = s.img[i];
     __syncthreads();
+    const DevTri48* tris = SMALL ? reinterpret_cast<const DevTri48*>(s_img + s.img_tri) : s.tris48;
+    const float4* lboxes = SMALL ? s_img + s.img_lb : s.leafbox;
     int slice = io.fetch8 ? (int)(blockIdx.x & 7u) : 0, tried = 0;  // wave-uniform
     unsigned s_len = __builtin_amdgcn_readfirstlane(s_tab[2][slice]);
     bool drained = false;                   // wave-uniform
@@ -218,7 +229,7 @@ void k_trace(SceneView s, TraceIO io) {
                 if (COUNT) (anyr ? c_stris : c_tris) += 1;
                 capture(1u, (unsigned)tri);
                 float t, u, v;
-                const bool hit = tri_intersect48p(s.tris48 + tri, o, d, [&](float tt) {
+                const bool hit = tri_intersect48p(tris + tri, o, d, [&](float tt) {
                     return anyr ? (tt < tbest && tt > RTG_EPS) : (tt <= tbest && tt > RTG_EPS);
                 }, t, u, v, c_tails);
                 if (hit) {
@@ -227,7 +238,7 @@ void k_trace(SceneView s, TraceIO io) {
                     if (cand && wide) {
                         // the exact box of the reference leaf holding this triangle (stored per
                         // triangle: a wide leaf slot may join sibling reference leaves)
-                        const float4 b0 = s.leafbox[2 * tri], b1 = s.leafbox[2 * tri + 1];
+                        const float4 b0 = lboxes[2 * tri], b1 = lboxes[2 * tri + 1];
                         if (COUNT) c_lbox += 1;
                         capture(2u, (unsigned)tri);
                         cand = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
@@ -251,7 +262,7 @@ void k_trace(SceneView s, TraceIO io) {
             float key[4];
             {
                 capture(0u, (unsigned)cur);
-                const float4* np = s.nodesq[cur].q;
+                const float4* np = SMALL ? s_img + 4 * cur : s.nodesq[cur].q;
                 const float4 h0 = np[0], h1 = np[1], h2 = np[2], h3 = np[3];
                 const unsigned ex = __float_as_uint(h0.w);
                 const float sx = __uint_as_float((ex & 255u) << 23);
@@ -326,7 +337,7 @@ void k_trace(SceneView s, TraceIO io) {
             // misses carry +inf and sort last
             if (key[0] == __builtin_inff()) {
                 cur = RTG_POP;
-            } else if (!COUNT && sp + 3 <= RTG_STACK) {
+            } else if (!COUNT && sp + 3 <= STK) {
                 // hits are a prefix of the sorted slots: push the h = hits - 1 far ones (far first)
                 // with three unconditional LDS writes; entries above sp + h are never read
                 const int h = (key[1] != __builtin_inff()) + (key[2] != __builtin_inff()) + (key[3] != __builtin_inff());
@@ -339,9 +350,9 @@ void k_trace(SceneView s, TraceIO io) {
 #pragma unroll
                 for (int k = 3; k >= 1; --k) {
                     if (key[k] != __builtin_inff()) {
-                        if (COUNT && sp < RTG_STACK) kstk[sp][tid] = key[k];
-                        if (sp < RTG_STACK) stk[sp][tid] = wd[k];
-                        else io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid] = wd[k];
+                        if (COUNT && sp < STK) kstk[sp][tid] = key[k];
+                        if (sp < STK) stk[sp][tid] = wd[k];
+                        else io.ovf[(size_t)(sp - STK) * gthreads + gtid] = wd[k];
                         ++sp;
                     }
                 }
@@ -363,9 +374,9 @@ void k_trace(SceneView s, TraceIO io) {
                 const bool lfirst = !(er < el);
                 const int nearw = lfirst ? nd.d.x : nd.d.y;
                 const int farw = lfirst ? nd.d.y : nd.d.x;
-                if (COUNT && sp < RTG_STACK) kstk[sp][tid] = -RTG_FLT_MAX;
-                if (sp < RTG_STACK) stk[sp][tid] = farw;
-                else io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid] = farw;
+                if (COUNT && sp < STK) kstk[sp][tid] = -RTG_FLT_MAX;
+                if (sp < STK) stk[sp][tid] = farw;
+                else io.ovf[(size_t)(sp - STK) * gthreads + gtid] = farw;
                 ++sp;
                 cur = nearw;
             } else if (hl) {
@@ -389,9 +400,9 @@ void k_trace(SceneView s, TraceIO io) {
                 cur = RTG_EXIT;
             } else {
                 --sp;
-                cur = stk[sp < RTG_STACK ? sp : 0][tid];
-                if (COUNT && !anyr && sp < RTG_STACK && kstk[sp][tid] > tbest) c_cullpop += 1;
-                if (sp >= RTG_STACK) cur = io.ovf[(size_t)(sp - RTG_STACK) * gthreads + gtid];
+                cur = stk[sp < STK ? sp : 0][tid];
+                if (COUNT && !anyr && sp < STK && kstk[sp][tid] > tbest) c_cullpop += 1;
+                if (sp >= STK) cur = io.ovf[(size_t)(sp - STK) * gthreads + gtid];
             }
         }
         // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on, or (the queue is
@@ -1113,17 +1124,32 @@ static size_t path_bytes(int planes, bool queues) { return (size_t)200 + (size_t
 static size_t slot_bytes(const ChunkSlot& sl) { return sl.cap_P * path_bytes(sl.cap_maxb, sl.pb.q[0] != nullptr); }
 
 #ifndef RTG_SLOT_STREAMS
-#define RTG_SLOT_STREAMS 2  // 0: plain streams, 1: one priority per slot, 2: full-CU-mask streams
+#define RTG_SLOT_STREAMS 2  // 0: plain streams, 1: one priority per slot, 2: full-CU-mask streams (pooled)
 #endif
+// Full-CU-mask slot streams, one set per device for the whole process: a stream with a CU mask gets
+// an HSA queue of its own (plain streams beyond GPU_MAX_HW_QUEUES share queues, and two slots on one
+// queue run in turn), but destroying such streams deadlocked the runtime after a few handles
+// (ROCm 7.2, tools/r04_churn.py), so they are created once and shared by the device's handles.
+static std::mutex g_slot_pool_mu;
+static std::map<int, std::array<hipStream_t, RTG_SLOTS>> g_slot_pool;
+static int pooled_slot_stream(rtg_handle* h, int k, hipStream_t* out) {
+    std::lock_guard<std::mutex> lock(g_slot_pool_mu);
+    auto it = g_slot_pool.find(h->device);
+    if (it == g_slot_pool.end()) it = g_slot_pool.emplace(h->device, std::array<hipStream_t, RTG_SLOTS>{}).first;
+    hipStream_t& s = it->second[k];
+    if (!s) {
+        std::vector<uint32_t> mask((h->n_cu + 31) / 32, 0xffffffffu);
+        if (h->n_cu % 32) mask.back() = (1u << (h->n_cu % 32)) - 1u;
+        HIPOK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    }
+    *out = s;
+    return RTG_OK;
+}
 static int ensure_stream(rtg_handle* h, ChunkSlot& sl) {
     if (!sl.stream) {
         const int k = (int)(&sl - h->slot);
         if (RTG_SLOT_STREAMS == 2) {
-            // a stream with a CU mask gets an HSA queue of its own: plain streams beyond
-            // GPU_MAX_HW_QUEUES share queues, and two slots on one queue run in turn
-            std::vector<uint32_t> mask((h->n_cu + 31) / 32, 0xffffffffu);
-            if (h->n_cu % 32) mask.back() = (1u << (h->n_cu % 32)) - 1u;
-            HIPOK(hipExtStreamCreateWithCUMask(&sl.stream, (uint32_t)mask.size(), mask.data()));
+            if (int rc = pooled_slot_stream(h, k, &sl.stream)) return rc;
         } else if (RTG_SLOT_STREAMS == 1) {
             int lo = 0, hi = 0;
             HIPOK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -1176,11 +1202,13 @@ int ensure_chunk(rtg_handle* h, ChunkSlot& sl, size_t P, int maxb, bool queues) 
 }
 
 int ensure_ovf(rtg_handle* h, ChunkSlot& sl) {
-    int grid = std::max(h->trace_blocks, h->trace_blocks_count);
+    int grid = std::max(std::max(h->trace_blocks, h->trace_blocks_count),
+                        std::max(h->trace_blocks_small, h->trace_blocks_small_count));
     // deepest stack: one entry per BVH2 level, or up to 3 per wide level (each wide level descends
-    // at least one BVH2 level)
+    // at least one BVH2 level); the small-scene variant keeps fewer entries in LDS
     size_t deep = std::max<size_t>(h->bvh_depth, (size_t)h->wide_depth * 3) + 2;
-    size_t levels = deep > RTG_STACK ? deep - RTG_STACK : 1;
+    const size_t lds = std::min(RTG_STACK, RTG_STACK_SMALL);
+    size_t levels = deep > lds ? deep - lds : 1;
     size_t need = levels * (size_t)grid * RTG_TTB;
     if (need <= sl.cap_ovf) return RTG_OK;
     if (sl.stream) HIPOK(hipStreamSynchronize(sl.stream));
@@ -1591,6 +1619,15 @@ int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
         float v = std::fabs(d->node_bounds[k]);
         if (std::isfinite(v)) scale = std::max(scale, v);
     }
+    // small scenes: the image k_trace<.., SMALL> copies into LDS (wide nodes | triangles | leaf boxes)
+    if (hs.usew && nodesq.size() * 4 + (size_t)nt * 5 <= RTG_SMALL_F4) {
+        hs.img.clear();
+        for (const DevNodeQ& q : nodesq) hs.img.insert(hs.img.end(), q.q, q.q + 4);
+        hs.img_tri = (int)hs.img.size();
+        for (const DevTri48& t : tris48) hs.img.insert(hs.img.end(), {t.a, t.b, t.c});
+        hs.img_lb = (int)hs.img.size();
+        hs.img.insert(hs.img.end(), leafbox.begin(), leafbox.begin() + (size_t)nt * 2);
+    }
     // ---- materials, textures, lights
     std::vector<DevMat> mats(d->n_materials);
     for (uint32_t i = 0; i < d->n_materials; ++i) {
@@ -1709,6 +1746,7 @@ int upload_scene(int device, const HostScene& hs, rtg_handle* h) {
     if ((rc = dev_upload(&h->d_nodes, hs.nodes))) return rc;
     if ((rc = dev_upload(&h->d_nodesq, hs.nodesq))) return rc;
     if ((rc = dev_upload(&h->d_leafbox, hs.leafbox))) return rc;
+    if (!hs.img.empty() && (rc = dev_upload(&h->d_img, hs.img))) return rc;
     if ((rc = dev_upload(&h->d_tris48, hs.tris48))) return rc;
     if ((rc = dev_upload(&h->d_shade, hs.shade))) return rc;
     if ((rc = dev_upload(&h->d_mats, hs.mats))) return rc;
@@ -1736,6 +1774,10 @@ int upload_scene(int device, const HostScene& hs, rtg_handle* h) {
     s.leafbox = h->d_leafbox;
     s.root_wordw = hs.root_wordw;
     s.usew = hs.usew ? 1 : 0;
+    s.img = hs.img.empty() ? nullptr : h->d_img;
+    s.img_n4 = (int)hs.img.size();
+    s.img_tri = hs.img_tri;
+    s.img_lb = hs.img_lb;
     for (int k = 0; k < 6; ++k) s.root_box[k] = hs.root_box[k];
     s.cull_scale = hs.cull_scale;
     h->cam = hs.cam;
@@ -1750,11 +1792,14 @@ int upload_scene(int device, const HostScene& hs, rtg_handle* h) {
     for (auto& e : h->ev) HIPOK(hipEventCreate(&e));
 
     int occ = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false>, RTG_TTB, 0));
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false, false>, RTG_TTB, 0));
     h->trace_blocks = h->n_cu * std::max(1, occ);
-    int occ3 = 0;
-    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ3, k_trace<true>, RTG_TTB, 0));
-    h->trace_blocks_count = h->n_cu * std::max(1, occ3);
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<true, false>, RTG_TTB, 0));
+    h->trace_blocks_count = h->n_cu * std::max(1, occ);
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<false, true>, RTG_TTB, 0));
+    h->trace_blocks_small = h->n_cu * std::max(1, occ);
+    HIPOK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_trace<true, true>, RTG_TTB, 0));
+    h->trace_blocks_small_count = h->n_cu * std::max(1, occ);
     HIPOK(hipEventCreateWithFlags(&h->entry, hipEventDisableTiming));
     return ensure_ovf(h, h->slot[0]);
 }
@@ -1787,9 +1832,10 @@ void rtg_destroy(rtg_handle* h) {
         free_chunk(sl);
         (void)hipFree(sl.d_ovf);
         if (sl.fold) (void)hipEventDestroy(sl.fold);
-        if (sl.stream) (void)hipStreamDestroy(sl.stream);
+        if (sl.stream && RTG_SLOT_STREAMS != 2) (void)hipStreamDestroy(sl.stream);  // (pooled: kept)
     }
     if (h->entry) (void)hipEventDestroy(h->entry);
+    (void)hipFree(h->d_img);
     (void)hipFree(h->d_nodes); (void)hipFree(h->d_nodesq); (void)hipFree(h->d_leafbox); (void)hipFree(h->d_tris48); (void)hipFree(h->d_shade); (void)hipFree(h->d_mats);
     (void)hipFree(h->d_lights); (void)hipFree(h->d_texinfo); (void)hipFree(h->d_texels); (void)hipFree(h->d_film);
     (void)hipFree(h->d_pix); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
@@ -1875,8 +1921,11 @@ int launch_generate(rtg_handle* h, const ChunkArgs& a, const PathBufs& pb, hipSt
 }
 
 int launch_trace(rtg_handle* h, const TraceIO& io, hipStream_t st) {
-    if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TTB), 0, st, h->sv, io);
-    else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, st, h->sv, io);
+    const bool small = h->sv.img != nullptr;
+    if (h->count && small) hipLaunchKernelGGL((k_trace<true, true>), dim3(h->trace_blocks_small_count), dim3(RTG_TTB), 0, st, h->sv, io);
+    else if (h->count) hipLaunchKernelGGL((k_trace<true, false>), dim3(h->trace_blocks_count), dim3(RTG_TTB), 0, st, h->sv, io);
+    else if (small) hipLaunchKernelGGL((k_trace<false, true>), dim3(h->trace_blocks_small), dim3(RTG_TTB), 0, st, h->sv, io);
+    else hipLaunchKernelGGL((k_trace<false, false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, st, h->sv, io);
     LAUNCH_OK("k_trace");
     return RTG_OK;
 }
@@ -1977,7 +2026,8 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     io.wide = h->wide;
     // RTG_DEBUG builds with RTG_OPT_WAVETIME: per-wave clocks of chunk 0's trace launches, on stderr
     unsigned long long* d_wt = nullptr;
-    const size_t wt_waves = (size_t)std::max(h->trace_blocks, h->trace_blocks_count) * (RTG_TTB / 64);
+    const size_t wt_waves = (size_t)std::max(std::max(h->trace_blocks, h->trace_blocks_count),
+                                             std::max(h->trace_blocks_small, h->trace_blocks_small_count)) * (RTG_TTB / 64);
     if (h->cap_cnt < maxb + 1) {
         if (h->h_cnt) (void)hipHostFree(h->h_cnt);
         h->h_cnt = nullptr;
@@ -2109,9 +2159,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                 io.cap_n = (unsigned)cn;
             }
             timed_begin(h, ss, k);
-            if (h->count) hipLaunchKernelGGL((k_trace<true>), dim3(h->trace_blocks_count), dim3(RTG_TTB), 0, ss, h->sv, io);
-            else hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, ss, h->sv, io);
-            LAUNCH_OK("k_trace");
+            if ((rc = launch_trace(h, io, ss))) return rc;
             timed_end(h, ss, k); kinds.push_back(0); ++k;
         }
         hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, ss, pb.ctr, maxb, h->d_stats);
@@ -2517,8 +2565,7 @@ static int trace_query(rtg_handle* h, const float* rays, uint32_t n, float* hits
         io.count = h->d_qctr;
         io.hits = (float4*)d_out;
     }
-    hipLaunchKernelGGL((k_trace<false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, h->stream, h->sv, io);
-    HIPOK(hipGetLastError());
+    if ((rc = launch_trace(h, io, h->stream))) return rc;
     HIPOK(hipStreamSynchronize(h->stream));
     if (any) HIPOK(hipMemcpy(vis, d_out, (size_t)n * sizeof(int), hipMemcpyDeviceToHost));
     else HIPOK(hipMemcpy(hits, d_out, (size_t)n * sizeof(float4), hipMemcpyDeviceToHost));

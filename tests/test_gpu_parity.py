@@ -693,3 +693,22 @@ def test_reference_side_binding_renders_reference_film(case):
         L.rtg_destroy(h)
     assert n.value == spp
     assert_bitexact(film, ref, "reference-side binding (%s)" % case)
+
+
+def test_handle_churn_with_queued_frames():
+    """Many handles created, rendering (waited-for and queued, one chunk at a time and several) and
+    destroyed in one process, as this suite does: destroying full-CU-mask streams deadlocked the HIP
+    runtime within a few handles (ROCm 7.2), so the slot streams are pooled per device."""
+    s = loadScene(os.path.join(SCENES, "cornell-mat"), width=64, height=35)
+    want = gpu_film(s, 3, seed=7, max_depth=8)
+    for i in range(60):
+        rt = RayTracer(s, seed=7, max_depth=8, max_paths=(300 if i % 3 == 0 else 0))
+        if i % 2:
+            rt.set_options(flags=rt.flags | N.RTG_OPT_SERIAL)
+        rt.render(2, first_sample=0)
+        rt.render(1, first_sample=2, sync=False)
+        film, n = rt.film()
+        assert n == 3
+        if i % 10 == 0:
+            assert_bitexact(film, want, "handle %d" % i)
+        del rt
