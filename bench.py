@@ -272,7 +272,7 @@ def main():
         step()
     # timed region: per-launch HIP events on the render stream give the closest-hit kernel time
     rt.set_options(flags=base | N.RTG_OPT_TIMING)
-    ext_rays = shadow_rays = paths = 0
+    ext_rays = shadow_rays = paths = cam_traced = 0
     extend_ms = shadow_ms = shade_ms = 0.0
     extend_launches = 0
     barrier_sync()
@@ -282,6 +282,7 @@ def main():
         st = rt.stats()
         timed_ranks = getattr(rt, "last_ranks", None)
         ext_rays += st["extension_rays"]
+        cam_traced += st["traced_camera_rays"]
         shadow_rays += st["shadow_rays"]
         paths += st["paths"]
         extend_ms += st["extend_ms"]
@@ -359,10 +360,16 @@ def main():
             solo.render(a.spp, first_sample=0)
             film_check = bool(np.array_equal(group_reduced.view(np.uint32), solo.film()[0].view(np.uint32)))
             del solo
+    # rays traced: renderTile's camera ray is the pixel centre's for every sample (Renderer.h:805-808),
+    # so the bounce-0 traversal traces one per pixel and the samples share its hit; the counts of
+    # the reference (extension_rays: one camera ray per sample) are what `value` is quoted on
+    def traced_ext(st_):
+        return st_["extension_rays"] - st_["paths"] + st_["traced_camera_rays"]
     totals = np.array([ext_rays, shadow_rays, paths, extend_ms, extend_launches,
-                       cs["node_visits"], cs["tri_tests"], cs["extension_rays"],
+                       cs["node_visits"], cs["tri_tests"], traced_ext(cs),
                        cw["node_visits"], cw["tri_tests"],
-                       cs["shadow_node_visits"], cs["shadow_tri_tests"], cs["shadow_rays"]], dtype=np.float64)
+                       cs["shadow_node_visits"], cs["shadow_tri_tests"], cs["shadow_rays"],
+                       ext_rays - paths + cam_traced], dtype=np.float64)
     t_max = elapsed
     if world > 1:
         import torch
@@ -373,8 +380,9 @@ def main():
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         t_max = float(te.item())
     (ext_rays, shadow_rays, paths, extend_ms, extend_launches, c_nodes, c_tris, c_ext, w_nodes, w_tris,
-     s_nodes, s_tris, c_sh) = totals.tolist()
+     s_nodes, s_tris, c_sh, ext_traced) = totals.tolist()
     rays = ext_rays + shadow_rays
+    rays_traced = ext_traced + shadow_rays
     mrays = rays / t_max / 1e6
     ms_step = t_max * 1e3 / a.steps
     if dropin is not None:
@@ -395,7 +403,7 @@ def main():
     # untimed counting pass) / the k_trace HIP-event time of the timed region. The 16-B request
     # form of the same roofline is kept as a sub-object.
     n_steps = a.steps
-    all_rays = cw["extension_rays"] + cw["shadow_rays"]
+    all_rays = traced_ext(cw) + cw["shadow_rays"]  # rays the traversal processed
     rec_step = cw["node_lane_steps"] + cw["tri_tests"] + cw["shadow_tri_tests"] + cw["leafbox_tests"]
     req_step = (4.0 * cw["node_lane_steps"] + 2.0 * (cw["tri_tests"] + cw["shadow_tri_tests"])
                 + cw["tri_tail_loads"] + 2.0 * cw["leafbox_tests"] + REQ_PER_RAY_IO * all_rays)
@@ -410,7 +418,8 @@ def main():
     s_tris_per_ray = s_tris / max(c_sh, 1)
     b_sray = 32.0 * s_boxes_per_ray + 36.0 * s_tris_per_ray + 48.0
     # time and rays both summed over ranks and launches
-    algo_gbs = (b_ray * ext_rays + b_sray * shadow_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
+    # (per traced ray: the counting pass's box / triangle tests over its traced rays)
+    algo_gbs = (b_ray * ext_traced + b_sray * shadow_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
     if world > 1:
         import torch
         rt_ = torch.tensor(req_totals, dtype=torch.float64, device=coll_dev)
@@ -472,6 +481,12 @@ def main():
             "ms_per_frame": round(ms_step / a.spp, 4),
             "mpaths_per_s": round(paths / t_max / 1e6, 2),
             "rays_per_path": round(rays / max(paths, 1), 4),
+            "rays_traced_per_path": round(rays_traced / max(paths, 1), 4),
+            "mrays_traced_per_s": round(rays_traced / t_max / 1e6, 2),
+            "rays_note": ("value counts the reference's rays: a camera ray per sample, as renderTile casts "
+                          "them (Renderer.h:805-808). That ray is the pixel centre's for every sample, so the "
+                          "traversal traces one per pixel per chunk and the samples share its hit (same film "
+                          "bits); rays_traced_per_path counts the rays traced"),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -555,9 +570,9 @@ def main():
                          "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from an own 3-axis SAH tree over the reference leaves)",
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
-                         "node_steps_per_ray": round(cw["node_lane_steps"] / max(cw["extension_rays"] + cw["shadow_rays"], 1), 2),
-                         "pops_per_ray": round(cw["pops"] / max(cw["extension_rays"], 1), 2),
-                         "cullable_pops_per_ray": round(cw["cullable_pops"] / max(cw["extension_rays"], 1), 2),
+                         "node_steps_per_ray": round(cw["node_lane_steps"] / max(all_rays, 1), 2),
+                         "pops_per_ray": round(cw["pops"] / max(traced_ext(cw), 1), 2),
+                         "cullable_pops_per_ray": round(cw["cullable_pops"] / max(traced_ext(cw), 1), 2),
                          # node: lanes stepping a node per loop iteration; leaf: lanes running a
                          # parked leaf per leaf phase; leaf phases per iteration
                          "lane_util_node_leaf": [round(cw["node_lane_steps"] / max(cw["lane_slots"], 1), 3),

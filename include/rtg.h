@@ -32,7 +32,8 @@ extern "C" {
 #endif
 
 /* 2: rtg_scene_desc.projection; 3: rtg_stats.tri_tail_loads / leafbox_tests appended;
- * 4: rtg_render_async queues frames (returns before any of its work has run), rtg_render_idle */
+ * 4: rtg_render_async queues frames (returns before any of its work has run), rtg_render_idle,
+ *    rtg_stats.traced_camera_rays appended */
 #define RTG_ABI_VERSION 4
 
 /* error codes */
@@ -120,6 +121,10 @@ typedef struct rtg_stats {
     uint64_t tri_tail_loads;       /* RTG_OPT_COUNT: triangle records whose last 16 B were fetched */
                                    /* (the plane distance was a candidate), all rays             */
     uint64_t leafbox_tests;        /* RTG_OPT_COUNT: reference leaf-box records fetched, all rays */
+    uint64_t traced_camera_rays;   /* path tracer: camera rays traced. renderTile's camera ray is the   */
+                                   /* pixel centre's for every sample (Renderer.h:805-808), so a chunk  */
+                                   /* traces one per pixel and its samples share the first hit;         */
+                                   /* extension_rays counts one per sample, as the reference casts them */
 } rtg_stats;
 
 typedef struct rtg_handle rtg_handle;

@@ -73,7 +73,8 @@ using namespace rtgd;
 // counters sharing a line serialise with each other.
 #define RTG_CPAD(f) unsigned f; unsigned f##_pad[31];
 struct __align__(16) Counters {
-    RTG_CPAD(n_ext) RTG_CPAD(n_shadow) RTG_CPAD(f_ext) RTG_CPAD(f_shadow) RTG_CPAD(f_shade) RTG_CPAD(pad0)
+    RTG_CPAD(n_ext) RTG_CPAD(n_shadow) RTG_CPAD(f_ext) RTG_CPAD(f_shadow) RTG_CPAD(f_shade)
+    RTG_CPAD(n_cam)  // path tracer, bounce 0: camera rays traced, one per pixel (k_generate)
     RTG_CPAD(pad1) RTG_CPAD(pad2)
     unsigned f8[8 * 32];  // sliced work counters of k_trace (TraceIO::fetch8), one 128-B line each
     // path tracer queues, segmented: k_shade block t appends to segment t % 8 (a device-scope atomic

@@ -571,16 +571,29 @@ void k_replay(SceneView s, const uint4* cap, const unsigned* cap_len, const unsi
 #endif
 
 // ------------------------------------------------------------------ generate
+// lean (the path tracer): one thread per pixel. renderTile's camera ray goes through the pixel centre
+// (Renderer.h:805-808: no jitter, a pinhole camera), so every sample of a pixel casts the same ray
+// and finds the same first hit: the bounce-0 traversal traces one ray per pixel (ray_d[lp],
+// hits[lp]) and k_shade's bounce 0 reads it for each of the pixel's samples. The rays counted in
+// rtg_stats stay the reference's (one per sample); traced_camera_rays counts the traced ones.
+// Otherwise (instant radiosity's camera pass, one sample): one thread per path, full path state.
 __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
     const unsigned pid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (a.seg_tiles && pid < 8) {  // path tracer: the camera rays as queue segments (positions = path ids)
+    if (a.seg_tiles && pid < 8) {  // path tracer: the paths as queue segments (positions = path ids)
         const unsigned cap = a.seg_tiles * RTG_TB, lo = pid * cap;
         p.ctr[0].ne8[32 * pid] = a.P > lo ? min(cap, a.P - lo) : 0u;
     }
+    if (a.seg_tiles && pid == 0) p.ctr[0].n_cam = a.npix;  // the bounce-0 traversal: a ray per pixel
     if (!a.seg_tiles && pid == 0) p.ctr[0].n_ext = a.P;  // instant radiosity's camera pass: one queue
-    if (pid >= a.P) return;
     unsigned lp, sl;  // pixel-major path ids
-    split_pid(a, pid, lp, sl);
+    if (a.lean) {
+        if (pid >= a.npix) return;
+        lp = pid;
+        sl = 0;
+    } else {
+        if (pid >= a.P) return;
+        split_pid(a, pid, lp, sl);
+    }
     const unsigned pixel = a.pixlist[lp];
     const unsigned W = (unsigned)a.cam.width;
     const unsigned x = pixel % W, y = pixel / W;
@@ -599,7 +612,7 @@ __global__ __launch_bounds__(RTG_TB) void k_generate(ChunkArgs a, PathBufs p) {
              (dir.x * c[4] + dir.y * c[5]) + dir.z * c[6],
              (dir.x * c[8] + dir.y * c[9]) + dir.z * c[10]);
     dir = normalize(dir);
-    p.ray_d[pid] = make_float4(dir.x, dir.y, dir.z, 0.0f);
+    p.ray_d[pid] = make_float4(dir.x, dir.y, dir.z, 0.0f);  // (lean: pid = lp)
     if (a.lean) return;  // the rest is implied at bounce 0 (k_trace: io.cam_o / identity queue; k_shade)
     p.ray_o[pid] = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f);
     p.q[0][pid] = pid;
@@ -680,9 +693,14 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
         float4 ro = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f), rd = ro, h = ro;
         DevShade S;
         if (valid) {
+            unsigned j = i;  // bounce 0: the pixel's camera ray and first hit (k_generate), shared by its samples
+            if (lean0) {
+                unsigned sl0;
+                split_pid(a, i, j, sl0);
+            }
             if (!lean0) ro = in_o[i];
-            rd = in_d[i];
-            h = p.hits[i];
+            rd = in_d[j];
+            h = p.hits[j];
             if (h.x < RTG_FLT_MAX) S = s.shade[__float_as_int(h.y)];
         }
         if (TAB) __syncthreads();  // (waits for the table loads: vmcnt(0))
@@ -1100,6 +1118,7 @@ __global__ void k_tally(const Counters* ctr, int maxb, unsigned long long* stats
     if (lane == 0) {
         atomicAdd(&stats[2], e);  // chunks in flight tally concurrently
         atomicAdd(&stats[3], sh);
+        atomicAdd(&stats[14], (unsigned long long)ctr[0].n_cam);  // camera rays traced (path tracer)
     }
 }
 
@@ -2077,7 +2096,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         if (hostgrid && !h->cstream) HIPOK(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
         HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), ss));
         timed_begin(h, ss, k);
-        hipLaunchKernelGGL(k_generate, dim3((a.P + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, ss, a, pb);
+        hipLaunchKernelGGL(k_generate, dim3((a.npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, ss, a, pb);  // lean: per pixel
         LAUNCH_OK("k_generate");
         timed_end(h, ss, k); kinds.push_back(2); ++k;
         // Trace launch L_b (b = 0..maxb) carries the extension rays of bounce b (from shade(b-1),
@@ -2122,10 +2141,11 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             io.ray_o = b == 0 ? nullptr : ((b & 1) ? pb.ray_o2 : pb.ray_o);
             io.cam_o = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f);
             io.ray_d = (b & 1) ? pb.ray_d2 : pb.ray_d;
-            // segmented queues (bounce 0: the P camera rays at identity positions, cut by k_generate)
-            io.count = nullptr;
-            io.seg_cap = a.seg_tiles * RTG_TB;
-            io.seg_ne = b < maxb ? pb.ctr[b].ne8 : nullptr;
+            // segmented queues; bounce 0: one queue of npix camera rays (a ray per pixel, shared by
+            // the pixel's samples) at identity positions, one work counter
+            io.count = b == 0 ? &pb.ctr[0].n_cam : nullptr;
+            io.seg_cap = b == 0 ? 0u : a.seg_tiles * RTG_TB;
+            io.seg_ne = (b > 0 && b < maxb) ? pb.ctr[b].ne8 : nullptr;
             io.seg_ns = b > 0 ? pb.ctr[b - 1].ns8 : nullptr;
             io.hits = pb.hits;
             io.squeue = pb.shq;
@@ -2137,7 +2157,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             io.contrib = b > 0 ? pb.contrib + (size_t)(b - 1) * a.P : nullptr;
             io.visible = nullptr;
             io.fetch = &pb.ctr[b].f_ext;
-            io.fetch8 = pb.ctr[b].f8;
+            io.fetch8 = b == 0 ? nullptr : pb.ctr[b].f8;
             io.wtime = (d_wt && c == 0) ? d_wt + (size_t)b * wt_waves * 3 : nullptr;
             io.cap = nullptr;
             io.cap_len = nullptr;
@@ -2510,6 +2530,7 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     h->stats.pops = c[12];
     h->stats.tri_tail_loads = c[6];
     h->stats.leafbox_tests = c[7];
+    h->stats.traced_camera_rays = c[14];
     *out = h->stats;
     return RTG_OK;
 }

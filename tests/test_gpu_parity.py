@@ -56,6 +56,19 @@ def test_c1_bit_exact_and_known_answer(cornell256):
     assert hashlib.md5((film / np.float32(4)).astype(np.float32).tobytes()).hexdigest() == kat
 
 
+def test_ray_counts_are_the_references_and_camera_rays_are_traced_per_pixel(cornell256):
+    """rtg_stats counts the reference's rays (C1: 702,961 closest-hit + 429,793 shadow rays for
+    262,144 paths, SURVEY.md §8d, the reference integrator's own counts), one camera ray per sample;
+    the traversal traces a camera ray per pixel per chunk (the pixel centre's, shared by the pixel's
+    samples: Renderer.h:805-808), so 4 spp in one chunk trace 65,536 and 4 chunks of 1 spp 262,144."""
+    for max_paths, traced in ((0, 256 * 256), (256 * 256, 4 * 256 * 256)):
+        rt = RayTracer(cornell256, seed=1234, max_paths=max_paths)
+        rt.render(4, first_sample=0)
+        s = rt.stats()
+        assert (s["paths"], s["extension_rays"], s["shadow_rays"]) == (262144, 702961, 429793), s
+        assert s["traced_camera_rays"] == traced
+
+
 def test_cull_is_exact(cornell256, synth20k):
     for s, spp in ((cornell256, 2), (synth20k, 2)):
         assert_bitexact(gpu_film(s, spp, cull=True), gpu_film(s, spp, cull=False), "cull vs no-cull")
