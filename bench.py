@@ -30,8 +30,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, same guide (§L2)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")  # rocprofv3 PMC passes of the C3 bench
-KSTATS = os.path.join(ROOT, "profiles", "r03_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")  # rocprofv3 PMC passes of the C3 bench
+KSTATS = os.path.join(ROOT, "profiles", "r04_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
 ROOF_REPLAY = os.path.join(ROOT, "profiles", "r03_roof_replay.jsonl")  # tools/roof_replay.py (C3)
 # the replay ceiling of each workload (tools/roof_replay.py on an MI355X), by (config, shard_of)
@@ -457,7 +457,7 @@ def main():
     shade_algo_gbs = shade_algo_bytes / (shade_ms / 1e3) / 1e9 if shade_ms > 0 else None
     shade_pmc = None
     if pmc:
-        ks = [v for k, v in pmc.get("kernels", {}).items() if k.startswith("void k_shade<false>")]
+        ks = [v for k, v in pmc.get("kernels", {}).items() if k.startswith("void k_shade<false")]
         if ks and ks[0].get("avg_ns_trace"):
             kb = ks[0]["read_bytes_corrected"] + ks[0]["write_bytes"]
             shade_pmc = {"bytes_per_launch": kb, "avg_launch_ms": round(ks[0]["avg_ns_trace"] / 1e6, 4),

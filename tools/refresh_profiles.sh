@@ -5,13 +5,13 @@
 # profiles/ afterwards.
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out/prof_out
-RND=${RND:-r02}
+RND=${RND:-r04}
 O=$R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_kt -o kt --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 2 > $O/prof_kt.log 2>&1 || { echo kt failed; tail -20 $O/prof_kt.log; exit 1; }
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/prof_fetch -o fetch --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 > $O/prof_fetch.log 2>&1 || { echo fetch failed; tail -20 $O/prof_fetch.log; exit 1; }
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $O/prof_write -o write --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 > $O/prof_write.log 2>&1 || { echo write failed; tail -20 $O/prof_write.log; exit 1; }
-timeout -k 10 400 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum -d $O/prof_dram -o dram --output-format csv -- python3 $R/bench.py --no-cpu-baseline --steps 1 --warmup 0 > $O/prof_dram.log 2>&1 || { echo dram failed; tail -20 $O/prof_dram.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_kt -o kt --output-format csv -- python3 $R/bench.py --no-cpu-baseline --dropin-frames 0 --steps 2 > $O/prof_kt.log 2>&1 || { echo kt failed; tail -20 $O/prof_kt.log; exit 1; }
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/prof_fetch -o fetch --output-format csv -- python3 $R/bench.py --no-cpu-baseline --dropin-frames 0 --steps 1 --warmup 0 > $O/prof_fetch.log 2>&1 || { echo fetch failed; tail -20 $O/prof_fetch.log; exit 1; }
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $O/prof_write -o write --output-format csv -- python3 $R/bench.py --no-cpu-baseline --dropin-frames 0 --steps 1 --warmup 0 > $O/prof_write.log 2>&1 || { echo write failed; tail -20 $O/prof_write.log; exit 1; }
+timeout -k 10 400 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum -d $O/prof_dram -o dram --output-format csv -- python3 $R/bench.py --no-cpu-baseline --dropin-frames 0 --steps 1 --warmup 0 > $O/prof_dram.log 2>&1 || { echo dram failed; tail -20 $O/prof_dram.log; exit 1; }
 cd $R
 python3 tools/pmc_summary.py $O/prof_fetch/fetch_counter_collection.csv $O/prof_write/write_counter_collection.csv $O/prof_kt/kt_kernel_stats.csv $O/prof_out/${RND}_pmc_traffic.json $O/prof_dram/dram_counter_collection.csv > /dev/null
 cp $O/prof_out/${RND}_pmc_traffic.json profiles/${RND}_pmc_traffic.json
