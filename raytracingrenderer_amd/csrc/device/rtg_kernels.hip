@@ -464,6 +464,7 @@ __global__ void k_cap_slices(TraceIO io, unsigned* tab) {
     for (int k = 0; k < 8; ++k) {
         unsigned elo, elen, len;
         trace_slice(io, nc, n, k, elo, elen, len);
+        if (!io.fetch8 && k > 0) elo = elen = len = 0;  // one work counter: a single slice (slice 0)
         tab[k] = elo;
         tab[8 + k] = elen;
         tab[16 + k] = elo;
@@ -1143,12 +1144,13 @@ static size_t path_bytes(int planes, bool queues) { return (size_t)200 + (size_t
 static size_t slot_bytes(const ChunkSlot& sl) { return sl.cap_P * path_bytes(sl.cap_maxb, sl.pb.q[0] != nullptr); }
 
 #ifndef RTG_SLOT_STREAMS
-#define RTG_SLOT_STREAMS 2  // 0: plain streams, 1: one priority per slot, 2: full-CU-mask streams (pooled)
+#define RTG_SLOT_STREAMS 1  // 0: plain streams, 1: one priority per slot, 2: full-CU-mask streams (pooled)
 #endif
-// Full-CU-mask slot streams, one set per device for the whole process: a stream with a CU mask gets
-// an HSA queue of its own (plain streams beyond GPU_MAX_HW_QUEUES share queues, and two slots on one
-// queue run in turn), but destroying such streams deadlocked the runtime after a few handles
-// (ROCm 7.2, tools/r04_churn.py), so they are created once and shared by the device's handles.
+// Plain streams beyond GPU_MAX_HW_QUEUES share HSA queues, and two slots on one queue run in turn
+// (queued 1-spp frames 2.93 ms each). Streams of different priorities (1) get queues of their own:
+// 2.28 ms. Full-CU-mask streams (2) also do (2.21 ms), but destroying them deadlocked the runtime
+// after a few handles (ROCm 7.2, tools/r04_churn.py), and kept alive in a per-device pool they
+// crashed the process at exit under rocprofv3; so (1).
 static std::mutex g_slot_pool_mu;
 static std::map<int, std::array<hipStream_t, RTG_SLOTS>> g_slot_pool;
 static int pooled_slot_stream(rtg_handle* h, int k, hipStream_t* out) {
