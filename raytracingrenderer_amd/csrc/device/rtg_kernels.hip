@@ -715,8 +715,14 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             split_pid(a, (unsigned)pid, lp, sl);
             const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);  // (carrying it in the payload: slower)
             uint64_t st = lean0 ? pcg_seed(a.seed, inc) : in_r[i];
-            v3 c;
+            v3 c = mk(0.0f, 0.0f, 0.0f);
             int nterms = b + 1;
+            // state carried past the environment lookup: a miss, or a path-traced hit (stage 1:
+            // its light sample taken, its shading, shadow ray and BSDF sample to come)
+            bool miss = false, env_need = false, env_light = false, spec = false;
+            int stage = 0, mid = 0;
+            v3 env_dir = d, x = o, sn = d, alb = d, l_p2 = o, l_em = d;
+            float l_g = 0.0f, l_pdf = 0.0f;
             if (ALT && a.mode == RTG_INTEGRATOR_DIRECT_MIS && b == 1) {
                 // computeDirectMIS, second half (Renderer.h:520-553): the BSDF-sampled ray's hit.
                 // thr = (bsdf value, bsdf pdf); scratch planes 2/3 = (x, light pdf * pmf) and
@@ -746,21 +752,22 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                 }
             } else if (!(h.x < RTG_FLT_MAX)) {
                 // miss: background->evaluate(r.dir), not weighted by throughput (Renderer.h:390);
-                // direct() and viewNormals() return black
-                c = (!ALT || a.mode == RTG_INTEGRATOR_PATH || a.mode == RTG_INTEGRATOR_ALBEDO) ? background(s, d)
-                                                                                             : mk(0.0f, 0.0f, 0.0f);
+                // direct() and viewNormals() return black. BackgroundColour(0) is black; an
+                // environment map is evaluated below, at the lane's one environment lookup.
+                env_need = (!ALT || a.mode == RTG_INTEGRATOR_PATH || a.mode == RTG_INTEGRATOR_ALBEDO) && s.env_tex >= 0;
+                miss = true;
             } else {
                 const float alpha = h.z, beta = h.w, gamma = 1.0f - (alpha + beta);
                 const float t = h.x;
-                const v3 x = add(o, muls(d, t));  // Ray::at
-                const DevMat& M = TAB ? s_mat[__float_as_int(S.d.w)] : s.mats[__float_as_int(S.d.w)];
+                x = add(o, muls(d, t));  // Ray::at
+                mid = __float_as_int(S.d.w);
+                const DevMat& M = TAB ? s_mat[mid] : s.mats[mid];
                 const v3 n0 = mk(S.a.x, S.a.y, S.a.z), n1 = mk(S.a.w, S.b.x, S.b.y), n2 = mk(S.b.z, S.b.w, S.c.x);
-                v3 sn = normalize(add(add(muls(n0, alpha), muls(n1, beta)), muls(n2, gamma)));
+                sn = normalize(add(add(muls(n0, alpha), muls(n1, beta)), muls(n2, gamma)));
                 const float tu = (S.c.y * alpha + S.c.w * beta) + S.d.y * gamma;
                 const float tv = (S.c.z * alpha + S.d.x * beta) + S.d.z * gamma;
                 const v3 wo = neg(d);
                 if (M.two_sided && dot(wo, sn) < 0) sn = neg(sn);
-                const frame fr = frame_from(sn);
                 if (ALT && a.mode == RTG_INTEGRATOR_NORMALS) {  // viewNormals (Renderer.h:572-582)
                     c = mk(fabsf(sn.x), fabsf(sn.y), fabsf(sn.z));
                 } else if (M.is_light) {
@@ -772,6 +779,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                 } else if (ALT && a.mode == RTG_INTEGRATOR_DIRECT_MIS) {
                     // computeDirectMIS, first half (Renderer.h:474-519): one light sample weighted by
                     // the balance heuristic (its shadow ray), then one BSDF sample (its extension ray)
+                    const frame fr = frame_from(sn);
                     c = mk(0.0f, 0.0f, 0.0f);
                     if (!(M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS)) {
                         const int nl = s.n_lights;
@@ -850,90 +858,103 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
                         nterms = 2;
                     }
                 } else {
-                    const bool spec = M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS;
+                    // computeDirect's light sample (Renderer.h:423-447); its shading, shadow ray and
+                    // the BSDF sample follow the lane's environment lookup below
+                    spec = M.kind == RTG_MAT_MIRROR || M.kind == RTG_MAT_GLASS;
                     // albedo->sample(tu, tv): one fetch for BSDF::evaluate (NEE) and BSDF::sample
-                    const v3 alb = tex_sample(s, M, tu, tv);
-                    // ---- computeDirect (Renderer.h:423-473)
-                    v3 ld = mk(0.0f, 0.0f, 0.0f);
-                    bool ld_pre = false;  // contrib takes the visible NEE value now
-                    v3 cpre = ld;
+                    alb = tex_sample(s, M, tu, tv);
                     if (!spec) {
                         const int nl = s.n_lights;
-                        const float pmf = s.pmf;  // 1.f / (float)nl
                         int li = (int)((float)nl * pcg_next(st, inc));
                         li = (nl - 1) < li ? (nl - 1) : li;  // (std::min)(a, b)
                         const DevLight L = TAB ? s_lt[li] : s.lights[li];
-                        v3 p2, wi;
-                        float g, pdf;
-                        v3 emitted;
                         if (__float_as_int(L.v1t.w) == 0) {  // AreaLight::sample -> Triangle::sample
                             const float r1 = pcg_next(st, inc);
                             const float r2 = pcg_next(st, inc);
                             const float la = 1 - sqrtf(r1);
                             const float lb = r2 * sqrtf(r1);
                             const float lg = 1.0f - (la + lb);
-                            pdf = L.v2.w;  // 1.0f / area
-                            p2 = add(add(muls(mk(L.v0a.x, L.v0a.y, L.v0a.z), la), muls(mk(L.v1t.x, L.v1t.y, L.v1t.z), lb)),
-                                     muls(mk(L.v2.x, L.v2.y, L.v2.z), lg));
-                            emitted = mk(L.em.x, L.em.y, L.em.z);
-                            wi = sub(p2, x);
+                            l_pdf = L.v2.w;  // 1.0f / area
+                            l_p2 = add(add(muls(mk(L.v0a.x, L.v0a.y, L.v0a.z), la), muls(mk(L.v1t.x, L.v1t.y, L.v1t.z), lb)),
+                                       muls(mk(L.v2.x, L.v2.y, L.v2.z), lg));
+                            l_em = mk(L.em.x, L.em.y, L.em.z);
+                            v3 wi = sub(l_p2, x);
                             const float l2 = length_sq(wi);
                             wi = normalize(wi);
-                            g = (wmax(dot(wi, sn), 0.0f) * wmax(-dot(wi, mk(L.gn.x, L.gn.y, L.gn.z)), 0.0f)) / l2;
+                            l_g = (wmax(dot(wi, sn), 0.0f) * wmax(-dot(wi, mk(L.gn.x, L.gn.y, L.gn.z)), 0.0f)) / l2;
                         } else {  // EnvironmentMap::sample: uniformSampleSphere(next(), next())
                             const float q2 = pcg_next(st, inc);  // evaluated first -> r2
                             const float q1 = pcg_next(st, inc);  // -> r1
-                            wi = uniform_sample_sphere(q1, q2);
-                            pdf = uniform_sphere_pdf();
-                            emitted = env_eval(s, wi);
-                            g = wmax(dot(wi, sn), 0.0f);
-                            p2 = add(x, muls(wi, 10000.0f));
-                        }
-                        if (g > 0) {
-                            // Scene::visible(x, p2)
-                            v3 sd = sub(p2, x);
-                            const float maxt = sqrtf(length_sq(sd)) - (2.0f * RTG_EPS);
-                            sd = normalize(sd);
-                            const v3 so = add(x, muls(sd, RTG_EPS));
-                            const v3 f = divs_pi(alb);  // BSDF::evaluate
-                            ld = divs(muls(mul(f, emitted), g), pmf * pdf);
-                            const v3 cvis = mul(thr, ld);
-                            s_sho[threadIdx.x] = make_float4(so.x, so.y, so.z, maxt);
-                            // Visible is the common case: contrib takes thr * Ld now and k_trace
-                            // writes thr * 0 = +0 on occlusion. When thr * 0 is not +0 (a non-finite
-                            // throughput) the value goes through sh_c and is copied on visibility.
-                            const v3 z = mul(thr, mk(0.0f, 0.0f, 0.0f));
-                            const bool plain = (__float_as_uint(z.x) | __float_as_uint(z.y) | __float_as_uint(z.z)) == 0u;
-                            s_shd[threadIdx.x] = make_float4(sd.x, sd.y, sd.z, plain ? 0.0f : 1.0f);
-                            if (!plain) p.sh_c[pid] = make_float4(cvis.x, cvis.y, cvis.z, 0.0f);
-                            ld_pre = plain;
-                            cpre = cvis;
-                            want_sh = true;
+                            const v3 wi = uniform_sample_sphere(q1, q2);
+                            l_pdf = uniform_sphere_pdf();
+                            l_g = wmax(dot(wi, sn), 0.0f);
+                            l_p2 = add(x, muls(wi, 10000.0f));
+                            env_dir = wi;  // its radiance: EnvironmentMap::evaluate(wi), below (used iff g > 0)
+                            env_need = l_g > 0;
+                            env_light = true;
                         }
                     }
-                    // direct = thr * Ld, with Ld = 0 until the shadow ray says visible
-                    c = ld_pre ? cpre : mul(thr, mk(0.0f, 0.0f, 0.0f));
-                    if ((!ALT || a.mode == RTG_INTEGRATOR_PATH) && b <= a.max_depth) {
-                        const float rrp = wmin(lum(thr), 0.9f);
-                        if (pcg_next(st, inc) < rrp) {
-                            thr = divs(thr, rrp);
-                            // ---- BSDF::sample
-                            v3 ind;
-                            float pdf;
-                            PcgSampler smp{st, inc};
-                            const v3 wi = bsdf_sample(M.kind, M.int_ior, M.ext_ior, alb, fr, wo,
-                                                      smp, ind, pdf);
-                            st = smp.s;
-                            if (spec) thr = divs(mul(thr, ind), pdf);
-                            else thr = divs(muls(mul(thr, ind), fabsf(dot(wi, sn))), pdf);
-                            const v3 no = add(x, muls(wi, RTG_EPS));
-                            n_o = make_float4(no.x, no.y, no.z, __int_as_float(pid));
-                            n_d = make_float4(wi.x, wi.y, wi.z, spec ? 1.0f : 0.0f);  // canHitLight
-                            want_ext = true;
-                            n_t = make_float4(thr.x, thr.y, thr.z, 0.0f);
-                            n_r = st;
-                            nterms = (b + 1) | ((spec ? 1 : 0) << 8);
-                        }
+                    stage = 1;
+                }
+            }
+            // The lane's one environment lookup: a miss's background and an environment light
+            // sample's radiance are the same EnvironmentMap::evaluate (Lights.h:150-157), so a wave
+            // holding both kinds of lane runs it once instead of in two divergent branches.
+            const v3 E = env_need ? env_eval(s, env_dir) : mk(0.0f, 0.0f, 0.0f);
+            if (miss) c = E;
+            if (stage == 1) {
+                const DevMat& M = TAB ? s_mat[mid] : s.mats[mid];
+                const v3 wo = neg(d);
+                const frame fr = frame_from(sn);
+                // ---- computeDirect (Renderer.h:423-473), after the light sample above
+                v3 ld = mk(0.0f, 0.0f, 0.0f);
+                bool ld_pre = false;  // contrib takes the visible NEE value now
+                v3 cpre = ld;
+                if (!spec && l_g > 0) {
+                    const float pmf = s.pmf;  // 1.f / (float)nl
+                    const v3 emitted = env_light ? E : l_em;
+                    // Scene::visible(x, p2)
+                    v3 sd = sub(l_p2, x);
+                    const float maxt = sqrtf(length_sq(sd)) - (2.0f * RTG_EPS);
+                    sd = normalize(sd);
+                    const v3 so = add(x, muls(sd, RTG_EPS));
+                    const v3 f = divs_pi(alb);  // BSDF::evaluate
+                    ld = divs(muls(mul(f, emitted), l_g), pmf * l_pdf);
+                    const v3 cvis = mul(thr, ld);
+                    s_sho[threadIdx.x] = make_float4(so.x, so.y, so.z, maxt);
+                    // Visible is the common case: contrib takes thr * Ld now and k_trace
+                    // writes thr * 0 = +0 on occlusion. When thr * 0 is not +0 (a non-finite
+                    // throughput) the value goes through sh_c and is copied on visibility.
+                    const v3 z = mul(thr, mk(0.0f, 0.0f, 0.0f));
+                    const bool plain = (__float_as_uint(z.x) | __float_as_uint(z.y) | __float_as_uint(z.z)) == 0u;
+                    s_shd[threadIdx.x] = make_float4(sd.x, sd.y, sd.z, plain ? 0.0f : 1.0f);
+                    if (!plain) p.sh_c[pid] = make_float4(cvis.x, cvis.y, cvis.z, 0.0f);
+                    ld_pre = plain;
+                    cpre = cvis;
+                    want_sh = true;
+                }
+                // direct = thr * Ld, with Ld = 0 until the shadow ray says visible
+                c = ld_pre ? cpre : mul(thr, mk(0.0f, 0.0f, 0.0f));
+                if ((!ALT || a.mode == RTG_INTEGRATOR_PATH) && b <= a.max_depth) {
+                    const float rrp = wmin(lum(thr), 0.9f);
+                    if (pcg_next(st, inc) < rrp) {
+                        thr = divs(thr, rrp);
+                        // ---- BSDF::sample
+                        v3 ind;
+                        float pdf;
+                        PcgSampler smp{st, inc};
+                        const v3 wi = bsdf_sample(M.kind, M.int_ior, M.ext_ior, alb, fr, wo,
+                                                  smp, ind, pdf);
+                        st = smp.s;
+                        if (spec) thr = divs(mul(thr, ind), pdf);
+                        else thr = divs(muls(mul(thr, ind), fabsf(dot(wi, sn))), pdf);
+                        const v3 no = add(x, muls(wi, RTG_EPS));
+                        n_o = make_float4(no.x, no.y, no.z, __int_as_float(pid));
+                        n_d = make_float4(wi.x, wi.y, wi.z, spec ? 1.0f : 0.0f);  // canHitLight
+                        want_ext = true;
+                        n_t = make_float4(thr.x, thr.y, thr.z, 0.0f);
+                        n_r = st;
+                        nterms = (b + 1) | ((spec ? 1 : 0) << 8);
                     }
                 }
             }
