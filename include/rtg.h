@@ -178,7 +178,7 @@ int  rtg_set_integrator(rtg_handle* h, int integrator);
  *   - with hip_stream NULL it is the drop-in RayTracer::render() of a frame loop (Main.cpp:74-118):
  *     the call is queued and returns before its work starts. Consecutive queued calls with the same
  *     seed and tiles whose samples follow on (frame f, f+1, ...) are coalesced and issued together
- *     once 16M paths are pending (16 frames of a 1-Mpixel film), or as soon as anything reads the
+ *     once 64M paths are pending (64 frames of a 1-Mpixel film), or as soon as anything reads the
  *     film or the stats, waits, or changes a setting (RTG_OPT_NO_COALESCE issues every call at
  *     once). Issued work of at most 16M paths per chunk runs in a pipeline of 3 slots, each with its
  *     own path state and stream, with no host wait: chunks run side by side on the GPU, a call waits

@@ -222,8 +222,8 @@ static int dev_upload(T** dst, const std::vector<T>& src) {
     return RTG_OK;
 }
 
-// Chunks in flight (the frame pipeline). A chunk of at most RTG_PIPE_MAX_P paths -- the coalesced
-// 1-spp frames of the drop-in RayTracer::render() (RTG_COALESCE_P) -- is issued without any host wait (its
+// Chunks in flight (the frame pipeline). A chunk of at most RTG_PIPE_MAX_P paths -- e.g. queued 1-spp
+// frames of the drop-in RayTracer::render() flushed before RTG_COALESCE_P -- is issued without any host wait (its
 // k_shade grids cover every tile a segment can hold; blocks past the live count exit at once) into the
 // next of RTG_SLOTS slots, each with its own path state, stack overflow and stream, so consecutive
 // frames run side by side on the GPU and fill each other's drain tails. The film folds stay in sample
@@ -237,7 +237,8 @@ static int dev_upload(T** dst, const std::vector<T>& src) {
 #define RTG_PIPE_MAX_P (16u << 20)
 #endif
 #ifndef RTG_COALESCE_P
-#define RTG_COALESCE_P (16u << 20)         // queued frames are issued once this many paths are pending
+#define RTG_COALESCE_P (64u << 20)         // queued frames are issued once this many paths are pending
+                                           // (64 frames of 1 Mpixel: one chunk, like the batched render)
 #endif
 #ifndef RTG_HOSTGRID_MIN_TILES
 #define RTG_HOSTGRID_MIN_TILES 4096u       // big chunks: seg_tiles at or above this size the k_shade grid
