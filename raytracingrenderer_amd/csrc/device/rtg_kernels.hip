@@ -27,8 +27,6 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
-#include <map>
-#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1165,34 +1163,17 @@ static size_t path_bytes(int planes, bool queues) { return (size_t)200 + (size_t
 static size_t slot_bytes(const ChunkSlot& sl) { return sl.cap_P * path_bytes(sl.cap_maxb, sl.pb.q[0] != nullptr); }
 
 #ifndef RTG_SLOT_STREAMS
-#define RTG_SLOT_STREAMS 1  // 0: plain streams, 1: one priority per slot, 2: full-CU-mask streams (pooled)
+#define RTG_SLOT_STREAMS 1  // 0: plain streams, 1: one priority per slot
 #endif
 // Plain streams beyond GPU_MAX_HW_QUEUES share HSA queues, and two slots on one queue run in turn
 // (queued 1-spp frames 2.93 ms each). Streams of different priorities (1) get queues of their own:
-// 2.28 ms. Full-CU-mask streams (2) also do (2.21 ms), but destroying them deadlocked the runtime
-// after a few handles (ROCm 7.2, tools/r04_churn.py), and kept alive in a per-device pool they
-// crashed the process at exit under rocprofv3; so (1).
-static std::mutex g_slot_pool_mu;
-static std::map<int, std::array<hipStream_t, RTG_SLOTS>> g_slot_pool;
-static int pooled_slot_stream(rtg_handle* h, int k, hipStream_t* out) {
-    std::lock_guard<std::mutex> lock(g_slot_pool_mu);
-    auto it = g_slot_pool.find(h->device);
-    if (it == g_slot_pool.end()) it = g_slot_pool.emplace(h->device, std::array<hipStream_t, RTG_SLOTS>{}).first;
-    hipStream_t& s = it->second[k];
-    if (!s) {
-        std::vector<uint32_t> mask((h->n_cu + 31) / 32, 0xffffffffu);
-        if (h->n_cu % 32) mask.back() = (1u << (h->n_cu % 32)) - 1u;
-        HIPOK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
-    }
-    *out = s;
-    return RTG_OK;
-}
+// 2.28 ms. (Full-CU-mask streams also do, 2.21 ms, but destroying them deadlocked the runtime after a
+// few handles (ROCm 7.2, tools/r04_churn.py) and kept alive in a per-device pool they crashed the
+// process at exit under rocprofv3: removed)
 static int ensure_stream(rtg_handle* h, ChunkSlot& sl) {
     if (!sl.stream) {
         const int k = (int)(&sl - h->slot);
-        if (RTG_SLOT_STREAMS == 2) {
-            if (int rc = pooled_slot_stream(h, k, &sl.stream)) return rc;
-        } else if (RTG_SLOT_STREAMS == 1) {
+        if (RTG_SLOT_STREAMS == 1) {
             int lo = 0, hi = 0;
             HIPOK(hipDeviceGetStreamPriorityRange(&lo, &hi));
             HIPOK(hipStreamCreateWithPriority(&sl.stream, hipStreamNonBlocking, k == 0 ? lo : k == 1 ? hi : (lo + hi) / 2));
@@ -1874,7 +1855,7 @@ void rtg_destroy(rtg_handle* h) {
         free_chunk(sl);
         (void)hipFree(sl.d_ovf);
         if (sl.fold) (void)hipEventDestroy(sl.fold);
-        if (sl.stream && RTG_SLOT_STREAMS != 2) (void)hipStreamDestroy(sl.stream);  // (pooled: kept)
+        if (sl.stream) (void)hipStreamDestroy(sl.stream);
     }
     if (h->entry) (void)hipEventDestroy(h->entry);
     (void)hipFree(h->d_img);
