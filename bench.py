@@ -41,15 +41,19 @@ ROOF_REPLAYS = {("C3", 1): ROOF_REPLAY,
                 ("C4", 1): os.path.join(ROOT, "profiles", "r04_roof_replay_c4_32spp.jsonl"),
                 ("C5", 1): os.path.join(ROOT, "profiles", "r04_roof_replay_c5_4spp.jsonl")}
 # k_shade's algorithmic bytes (PATH integrator; the payload travels with the queues):
-# every shaded path reads its direction 16, hit record 16, pixel 4 and, on a hit, the triangle's
-# shading record 64, and writes contrib 16 and meta 4; a path past the camera bounce also reads its
-# origin 16, throughput 16 and PCG state 8, which the previous shade wrote (16 + 16 + 16 + 8 with its
-# direction); an NEE sample writes sh_o, sh_d 16 each and the path id 4. Scene records shared by
-# many paths (materials, lights, texels) are not counted. The kernel time also holds k_generate (16 B
-# camera direction per path) and k_accumulate (reads each contrib entry 16 and meta 4 per path, the
-# film once): SHADE_B_CAM per path, and the contrib read-back in SHADE_B_PATH.
-SHADE_B_PATH = 16 + 16 + 4 + 64 + 16 + 4 + 16
-SHADE_B_CAM = 16 + 4
+# every shaded path reads its pixel 4 and writes contrib 16 and meta 4 (k_accumulate reads the contrib
+# entry back: 16); every traced closest-hit ray's direction 16, hit record 16 and, on a hit, the
+# triangle's shading record 64 are read once -- at the camera bounce once per pixel, since the samples
+# of a pixel share renderTile's pixel-centre ray and its hit (Renderer.h:805-808); a path past the
+# camera bounce also reads its origin 16, throughput 16 and PCG state 8, which the previous shade
+# wrote (16 + 16 + 16 + 8 with its direction); an NEE sample writes sh_o, sh_d 16 each and the path
+# id 4. Scene records shared by many paths (materials, lights, texels) are not counted. The kernel
+# time also holds k_generate (16 B per traced camera ray) and k_accumulate (meta 4 per path, the
+# film once).
+SHADE_B_PATH = 4 + 16 + 4 + 16
+SHADE_B_HIT = 16 + 16 + 64
+SHADE_B_CAM = 16
+SHADE_B_META = 4
 SHADE_B_CONT = (16 + 16 + 8) + (16 + 16 + 16 + 8)
 SHADE_B_NEE = 16 + 16 + 4
 ROOF_TABLE_MIB = 69  # the hot scene of C3: 21 MB wide nodes + 48 MB triangle records
@@ -452,7 +456,8 @@ def main():
     # generate + shade + accumulate HIP events), and the PMC DRAM-level bytes of its launches
     shaded = ext_rays  # every closest-hit ray's result is shaded once
     cont = max(ext_rays - paths, 0)  # continuing paths = extension rays after the camera rays
-    shade_algo_bytes = (shaded * SHADE_B_PATH + cont * SHADE_B_CONT + shadow_rays * SHADE_B_NEE + paths * SHADE_B_CAM
+    shade_algo_bytes = (shaded * SHADE_B_PATH + (cont + cam_traced) * SHADE_B_HIT + cont * SHADE_B_CONT
+                        + shadow_rays * SHADE_B_NEE + cam_traced * SHADE_B_CAM + paths * SHADE_B_META
                         + 12.0 * a.width * a.height * 2 * a.steps)
     shade_algo_gbs = shade_algo_bytes / (shade_ms / 1e3) / 1e9 if shade_ms > 0 else None
     shade_pmc = None
@@ -583,11 +588,13 @@ def main():
                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": None if shade_algo_gbs is None else round(shade_algo_gbs / HBM_PEAK_GBS, 4),
                                "algorithmic_bytes_per_step": round(shade_algo_bytes / max(a.steps, 1)),
-                               "definition": "per shaded path %d B (direction, hit, pixel, shading record reads; contrib/meta "
-                                             "writes), +%d B per path past the camera bounce (its payload written by one "
-                                             "shade, read by the next), +%d B per NEE sample; scene records shared by "
-                                             "paths not counted; + %d B per path for k_generate / k_accumulate and the film read + write"
-                                             % (SHADE_B_PATH, SHADE_B_CONT, SHADE_B_NEE, SHADE_B_CAM),
+                               "definition": "per shaded path %d B (pixel read, contrib/meta writes, contrib read-back), "
+                                             "+%d B per traced closest-hit ray (direction, hit, shading record: at the camera "
+                                             "bounce once per pixel, shared by its samples), +%d B per path past the camera "
+                                             "bounce (its payload written by one shade, read by the next), +%d B per NEE sample; "
+                                             "scene records shared by paths not counted; + %d B per traced camera ray (k_generate), "
+                                             "%d B per path (k_accumulate's meta) and the film read + write"
+                                             % (SHADE_B_PATH, SHADE_B_HIT, SHADE_B_CONT, SHADE_B_NEE, SHADE_B_CAM, SHADE_B_META),
                                "pmc": shade_pmc,
                                "pmc_source": (None if shade_pmc is None else "%s (k_shade<false>, DRAM-level bytes "
                                               "FETCH_SIZE x2 + WRITE_SIZE per launch, rocprof kernel-trace duration); "
