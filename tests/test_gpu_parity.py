@@ -244,6 +244,23 @@ def test_queued_frames_return_early_and_equal_one_render(tmp_path, coalesce):
     assert st["paths"] == 12 * 1024 * 1024
 
 
+def test_queued_frames_past_the_coalescing_threshold(cornell256):
+    """Queued 1-spp frames of a 256x256 film reach the coalescing threshold (64M paths = 1024
+    frames) inside the loop: the call that reaches it issues one chunk larger than the pipeline's
+    (slot 0, read-back grid), the frames after it queue again, and the film is bit-identical to one
+    rtg_render of all the samples."""
+    n = 1100
+    full = gpu_film(cornell256, n, seed=7)
+    rt = RayTracer(cornell256, seed=7)
+    for f in range(n):
+        rt.render(1, first_sample=f, sync=False)
+    assert rt.getSPP() == n
+    film, spp = rt.film()
+    assert spp == n
+    assert_bitexact(film, full, "%d queued 1-spp frames vs one %d-spp render" % (n, n))
+    assert rt.stats()["paths"] == n * 256 * 256
+
+
 @pytest.mark.parametrize("name", ["cornell256", "synth20k"])
 @pytest.mark.parametrize("cull", [True, False])
 def test_ray_queries_match_reference(name, cull, cornell256, synth20k):
