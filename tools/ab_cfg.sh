@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of the lib variants in raytracingrenderer_amd/lib/ab over several configs, 2 interleaved rounds:
-# C3 (headline), C2, C4 at 64 spp, C5 at 32 spp. Prints value and kernel ms per step.
+# C3 (headline), C2, C4 at 64 spp, C5 at 32 spp, S8 (rank 0's C3 share at 8 ranks). Prints value and kernel ms per step.
 R=$GRAFT_REPO_ROOT; mkdir -p $R/gpurun_out; cd $R
 CFGS=${CFGS:-"C3 C2 C4 C5"}
 for round in 1 2; do
@@ -11,6 +11,7 @@ for lib in raytracingrenderer_amd/lib/ab/*.so; do
     C2) args="--config C2 --steps 20 --warmup 2";;
     C4) args="--config C4 --spp 64 --steps 2 --warmup 1";;
     C5) args="--config C5 --spp 32 --steps 2 --warmup 1";;
+    S8) args="--shard-of 8 --steps 30 --warmup 3";;
   esac
   RTG_LIB=$R/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --dropin-frames 0 $args > gpurun_out/ab.log 2> gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 1; }
   echo "$cfg $(basename $lib) $(tail -1 gpurun_out/ab.log | python3 -c "
