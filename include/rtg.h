@@ -183,8 +183,10 @@ int  rtg_set_integrator(rtg_handle* h, int integrator);
  *     once). Issued work of at most 16M paths per chunk runs in a pipeline of 3 slots, each with its
  *     own path state and stream, with no host wait: chunks run side by side on the GPU, a call waits
  *     only for the chunk three before it to leave the GPU, and the film updates stay in sample
- *     order, so the film is bit-identical to one rtg_render of all the samples. Larger chunks read
- *     each bounce's live count back during the traversal. rtg_film_read with a film pointer,
+ *     order, so the film is bit-identical to one rtg_render of all the samples. Larger chunks (the
+ *     call that reaches the 64M threshold issues one) read each bounce's live count back during the
+ *     traversal, so that call returns once the chunk's last bounce is issued; the calls before it
+ *     return at once. rtg_film_read with a film pointer,
  *     rtg_film_copy_device, rtg_get_stats, rtg_synchronize, rtg_render_idle, rtg_clear ... first
  *     issue and wait for the queued calls; rtg_film_read(h, NULL, &spp) returns Film::SPP at once.
  *     An error of a coalesced call is reported by the call that issues it.
