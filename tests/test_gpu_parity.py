@@ -5,6 +5,7 @@ import ctypes as C
 import hashlib
 import json
 import os
+import zlib
 
 import numpy as np
 import pytest
@@ -472,6 +473,59 @@ def test_coincident_triangles_tree_rebuild(tmp_path, n_copies):
     rt = RayTracer(s)
     assert_bitexact(rt.trace_closest(r), o.trace_closest(r), "coincident closest")
     assert np.array_equal(rt.trace_visible(r), o.trace_visible(r))
+
+
+def _random_mesh(kind, rng):
+    """Geometry families that stress the compressed walk's conservative boxes, the exact leaf gate
+    and the BVH2 fallback: (n, 3, 3) float32 triangle positions around the origin."""
+    if kind == "small":  # the C3 recipe at a smaller count
+        c = rng.uniform(-1, 1, (3000, 1, 3))
+        return (c + rng.uniform(-0.03, 0.03, (3000, 3, 3))).astype(np.float32)
+    if kind == "large":  # big, heavily overlapping triangles
+        return rng.uniform(-1.2, 1.2, (300, 3, 3)).astype(np.float32)
+    if kind == "slivers":  # long needles, 1e-3 wide: near-degenerate edges, large 1/area
+        a = rng.uniform(-1, 1, (6000, 1, 3))
+        c = a + rng.uniform(-0.6, 0.6, (6000, 1, 3))
+        b = c + rng.uniform(-1e-3, 1e-3, (6000, 1, 3))
+        return np.concatenate([a, b, c], 1).astype(np.float32)
+    if kind == "axis_planes":  # triangles lying in x / y / z = const planes (flat boxes, dead slabs)
+        P = rng.uniform(-1, 1, (1500, 3, 3))
+        ax = rng.integers(0, 3, 1500)
+        P[np.arange(1500), :, ax] = np.round(rng.uniform(-1, 1, 1500), 1)[:, None]
+        return P.astype(np.float32)
+    if kind == "grid":  # a heightfield: triangles sharing edges and vertices
+        n = 48
+        x, y = np.meshgrid(np.linspace(-1, 1, n), np.linspace(-1, 1, n))
+        z = 0.2 * np.sin(3 * x) * np.cos(2 * y)
+        V = np.stack([x, y, z], -1)
+        a, b, c, d = V[:-1, :-1], V[1:, :-1], V[:-1, 1:], V[1:, 1:]
+        T = np.concatenate([np.stack([a, b, d], -2).reshape(-1, 3, 3), np.stack([a, d, c], -2).reshape(-1, 3, 3)])
+        return T.astype(np.float32)
+    if kind == "huge_scale":  # coordinates of 1e4: the camera sits inside the geometry
+        c = rng.uniform(-1, 1, (1000, 1, 3)) * 1e4
+        return (c + rng.uniform(-300, 300, (1000, 3, 3))).astype(np.float32)
+    if kind == "tiny_tris":  # 50k triangles a few 1e-3 across: leaves far below a pixel
+        c = rng.uniform(-0.7, 0.7, (50000, 1, 3))
+        return (c + rng.uniform(-3e-3, 3e-3, (50000, 3, 3))).astype(np.float32)
+    if kind == "duplicates":  # every triangle twice (equal hit distances: ties by index)
+        c = rng.uniform(-1, 1, (600, 1, 3))
+        T = (c + rng.uniform(-0.1, 0.1, (600, 3, 3))).astype(np.float32)
+        return np.concatenate([T, T[::-1]], 0)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind,depth", [("small", 4), ("large", 8), ("slivers", 4), ("axis_planes", 6),
+                                        ("grid", 8), ("huge_scale", 4), ("tiny_tris", 4), ("duplicates", 5)])
+def test_adversarial_meshes_render_like_the_oracle(tmp_path, kind, depth):
+    """Whole renders (environment-lit C3 recipe, 64x64, 3 spp) of geometry families that stress the
+    traversal's exactness: the GPU film equals the C oracle's bit for bit."""
+    from raytracingrenderer_amd.renderer import write_mesh_scene
+    rng = np.random.default_rng(zlib.crc32(kind.encode()))
+    P = _random_mesh(kind, rng)
+    s = loadScene(write_mesh_scene(str(tmp_path), P, 64, 64))
+    film = gpu_film(s, 3, seed=77, max_depth=depth)
+    ref, _ = Oracle(s, depth, "rtm").render(3, seed=77, threads=8)
+    assert_bitexact(film, ref, "%s depth %d" % (kind, depth))
 
 
 def test_adaptive_render_matches_oracle():
