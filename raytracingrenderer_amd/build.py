@@ -14,6 +14,7 @@ Every float-producing unit is compiled with -ffp-contract=off (bit-faithful arit
 import os
 import shutil
 import subprocess
+import tempfile
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -26,7 +27,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RTG_ARCH", "gfx950")
 
 HOST_SRC = ["host/image_io.cpp", "host/jpeg_decode.cpp", "host/gem_json.cpp", "host/scene_front.cpp"]
-DEVICE_SRC = ["device/rtg_kernels.hip", "device/rtg_light.hip", "device/rtg_multi.hip"]
+DEVICE_SRC = ["device/rtg_kernels.hip", "device/rtg_shade.hip", "device/rtg_light.hip", "device/rtg_multi.hip"]
+# per-unit compile flags: k_shade's translation unit takes LLVM's max-ilp scheduler, which its
+# latency-bound body prefers, while the traversal keeps the default
+DEVICE_FLAGS = {"device/rtg_shade.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 
 
 def _newer(out, deps):
@@ -68,9 +72,22 @@ def build_device(force=False, debug=False):
     out = os.path.join(d, "librtg.so")
     src = [os.path.join(CSRC, s) for s in DEVICE_SRC]
     if force or _newer(out, _deps(src)):
-        _run([HIPCC, "--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-std=c++17",
-              "-fPIC", "-shared"] + (["-DRTG_DEBUG=1"] if debug else []) + ["-o", out] + src +
-             ["-ldl", "-Wl,-rpath,/opt/rocm/lib"])
+        # one object per unit (each with its own flags, compiled in parallel), then one link
+        with tempfile.TemporaryDirectory() as tmp:
+            objs, procs = [], []
+            for rel, path in zip(DEVICE_SRC, src):
+                obj = os.path.join(tmp, os.path.basename(rel) + ".o")
+                cmd = ([HIPCC, "--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-std=c++17", "-fPIC"] +
+                       (["-DRTG_DEBUG=1"] if debug else []) + DEVICE_FLAGS.get(rel, []) + ["-c", "-o", obj, path])
+                procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+                objs.append(obj)
+            for cmd, pr in procs:
+                log = pr.communicate()[0]
+                if pr.returncode != 0:
+                    sys.stderr.write(log)
+                    raise RuntimeError("build failed: " + " ".join(cmd))
+            _run([HIPCC, "--offload-arch=" + ARCH, "-fPIC", "-shared", "-o", out] + objs +
+                 ["-ldl", "-Wl,-rpath,/opt/rocm/lib"])
     return out
 
 

@@ -368,3 +368,6 @@ int join_frames(rtg_handle* h);
 int launch_generate(rtg_handle* h, const ChunkArgs& a, const PathBufs& pb, hipStream_t st);
 // one k_trace launch (closest-hit rays of io.queue and any-hit rays of io.squeue) on stream st
 int launch_trace(rtg_handle* h, const TraceIO& io, hipStream_t st);
+// rtg_shade.hip: one k_shade launch of `grid` blocks (ALT = alt, TAB = tab) for bounce b
+int launch_shade(bool alt, bool tab, unsigned grid, hipStream_t st, const SceneView& s, const ChunkArgs& a,
+                 const PathBufs& p, int b);

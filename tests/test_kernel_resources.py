@@ -9,7 +9,7 @@ import tempfile
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "raytracingrenderer_amd", "csrc", "device", "rtg_kernels.hip")
+DEVICE = os.path.join(ROOT, "raytracingrenderer_amd", "csrc", "device")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
@@ -17,17 +17,21 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 def kernels():
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
-    with tempfile.TemporaryDirectory() as d:
-        out = os.path.join(d, "k.s")
-        subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17",
-                        "--cuda-device-only", "-S", "-o", out, SRC], check=True, capture_output=True)
-        s = open(out).read()
-    md = s[s.index("amdhsa.kernels"):]
+    from raytracingrenderer_amd.build import DEVICE_FLAGS  # each unit with the flags the build uses
     res = {}
-    for blk in md.split("  - .agpr_count")[1:]:
-        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
-        res[name] = {k: int(re.search(r"\." + k + r":\s+(\d+)", blk).group(1))
-                     for k in ("vgpr_count", "vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size")}
+    for rel in ("device/rtg_kernels.hip", "device/rtg_shade.hip"):
+        with tempfile.TemporaryDirectory() as d:
+            out = os.path.join(d, "k.s")
+            subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"] +
+                           DEVICE_FLAGS.get(rel, []) + ["--cuda-device-only", "-S", "-o", out,
+                                                        os.path.join(DEVICE, os.path.basename(rel))],
+                           check=True, capture_output=True)
+            s = open(out).read()
+        md = s[s.index("amdhsa.kernels"):]
+        for blk in md.split("  - .agpr_count")[1:]:
+            name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+            res[name] = {k: int(re.search(r"\." + k + r":\s+(\d+)", blk).group(1))
+                         for k in ("vgpr_count", "vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size")}
     return res
 
 
