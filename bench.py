@@ -32,6 +32,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, same guide (§L2)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")  # rocprofv3 PMC passes of the C3 bench
 KSTATS = os.path.join(ROOT, "profiles", "r04_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
+VALU_ISSUE = os.path.join(ROOT, "profiles", "r04_valu_issue.json")    # tools/valu_issue.py (SQ_INSTS_VALU passes)
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
 ROOF_REPLAY = os.path.join(ROOT, "profiles", "r04_roof_replay.jsonl")  # tools/roof_replay.py (C3)
 # the replay ceiling of each workload (tools/roof_replay.py on an MI355X), by (config, shard_of)
@@ -468,6 +469,24 @@ def main():
             shade_pmc = {"bytes_per_launch": kb, "avg_launch_ms": round(ks[0]["avg_ns_trace"] / 1e6, 4),
                          "achieved_gbs": round(kb / (ks[0]["avg_ns_trace"] / 1e9) / 1e9, 1)}
 
+    # VALU issue of the two hot kernels against the chip's wave64 issue peak (C3 PMC passes, profiles/)
+    valu = {}
+    if profiled and os.path.exists(VALU_ISSUE):
+        try:
+            vj = json.load(open(VALU_ISSUE))
+            for key, name in (("trace", "k_trace<false, false>"), ("shade", "k_shade<false, ...>")):
+                kv = vj["kernels"].get(name)
+                if kv:
+                    valu[key] = {"achieved": kv["achieved_g_per_s"], "peak": vj["peak_g_per_s"],
+                                 "unit": "G wave64 VALU instructions/s", "frac": kv["frac"],
+                                 "per_wave": kv["valu_per_wave"],
+                                 "source": "%s: SQ_INSTS_VALU over the kernel's dispatch time, rocprofv3 --pmc; peak "
+                                           "= 256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 instruction "
+                                           "(MI355X_MICROARCH.md); from profiles/, not measured in this run"
+                                           % os.path.relpath(VALU_ISSUE, ROOT)}
+        except Exception:
+            valu = {}
+
     cpu = None
     if rank == 0 and world == 1 and group_devs is None and not a.no_cpu_baseline:
         cpu = cpu_baseline(scene, a, work)
@@ -572,6 +591,7 @@ def main():
                                           "per_ray": round(req_step / max(all_rays, 1), 2)},
                              "tri_tail_loads_per_ray": round(cw["tri_tail_loads"] / max(all_rays, 1), 2),
                              "leafbox_tests_per_ray": round(cw["leafbox_tests"] / max(all_rays, 1), 2)},
+                         "valu": valu.get("trace"),
                          "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from an own 3-axis SAH tree over the reference leaves)",
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
@@ -595,6 +615,7 @@ def main():
                                              "scene records shared by paths not counted; + %d B per traced camera ray (k_generate), "
                                              "%d B per path (k_accumulate's meta) and the film read + write"
                                              % (SHADE_B_PATH, SHADE_B_HIT, SHADE_B_CONT, SHADE_B_NEE, SHADE_B_CAM, SHADE_B_META),
+                               "valu": valu.get("shade"),
                                "pmc": shade_pmc,
                                "pmc_source": (None if shade_pmc is None else "%s (k_shade<false>, DRAM-level bytes "
                                               "FETCH_SIZE x2 + WRITE_SIZE per launch, rocprof kernel-trace duration); "
