@@ -4,14 +4,19 @@ vs peak" on config C3 (synthetic 1M random triangles, 1024x1024, 64 spp, MAX_DEP
 
 One step = one complete 1024x1024x64spp render (64 RayTracer::render() frames) of this rank's
 32x32 tiles ((tile_x + tile_y) % world_size == rank) through the HIP wavefront tracer, plus, for N > 1, the
-RCCL reduce(sum) of the float32 radiance film to rank 0 over xGMI (tile supports are disjoint, so
-the reduced film is bit-identical to a 1-GPU render). Total work is fixed as N grows (strong
-scaling). Scene generation, loading and BVH build happen before the timed region.
+own-tile film exchange to rank 0 over xGMI (every rank packs its tiles' pixels, one RCCL gather,
+rank 0 scatters them; tile supports are disjoint and cover the film, so the assembled film is
+bit-identical to a 1-GPU render). Total work is fixed as N grows (strong scaling). Scene
+generation, loading and BVH build happen before the timed region.
+
+`value` is traced rays per second (closest-hit + shadow rays the traversal walked): renderTile casts
+the pixel-centre camera ray for every sample (Renderer.h:805-808), the GPU traces it once per pixel
+per chunk, and `mrays_reference_equivalent_per_s` counts it once per sample as the reference does.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
       N > 1 without torchrun: one process drives N GPUs through the native group (rtg_group_*:
-      one handle and host thread per device, ncclCommInitAll + ncclReduce of the film), the path an
-      RTBase C++ host takes. N must not exceed the visible devices (exit status 2 otherwise).
+      one handle and host thread per device, ncclCommInitAll + the own-tile exchange of the film),
+      the path an RTBase C++ host takes. N must not exceed the visible devices (exit status 2 otherwise).
   python bench.py --devices 0,0 [--verify-film]
       the same group path over an explicit device list; repeats rehearse N ranks on one GPU
   torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL via torch)
@@ -100,7 +105,7 @@ def scene_dir(name):
 class GroupRender:
     """The native one-process group (RayTracerGroup: rtg_group_* in rtg_multi.hip) behind the calls
     bench.py makes on a RayTracer: render = every rank renders its diagonal tile stripes on its own
-    device (one host thread each), then the RCCL film reduce into devices[0]; stats are summed over
+    device (one host thread each), then the own-tile film exchange into devices[0]; stats are summed over
     the ranks."""
 
     def __init__(self, scene, devices, max_depth, max_paths):
@@ -193,7 +198,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    # RTG_DIST_BACKEND=gloo rehearses the N>1 path on one GPU (ranks share cuda:0, the film reduce
+    # RTG_DIST_BACKEND=gloo rehearses the N>1 path on one GPU (ranks share cuda:0, the film exchange
     # goes through host memory); the default is RCCL ("nccl"), one GPU per rank
     backend = os.environ.get("RTG_DIST_BACKEND", "nccl")
     if world > 1:
@@ -234,7 +239,7 @@ def main():
         scene = loadScene(work, width=a.width, height=a.height,
                           skip_missing=cfg.get("skip_missing", False), envmap=cfg.get("envmap"))
     setup_s = time.time() - t0
-    from raytracingrenderer_amd.distributed import reduce_film, tiles_for_rank
+    from raytracingrenderer_amd.distributed import FilmExchange, tiles_for_rank
     if group_devs is not None:
         rt = GroupRender(scene, group_devs, a.max_depth, a.max_paths)
         tiles = None  # the group partitions the tiles itself (rtg_tiles_for_rank)
@@ -244,23 +249,27 @@ def main():
         if a.shard_of > 1 and world == 1:
             tiles = tiles_for_rank(a.width, a.height, 0, a.shard_of)
 
-    film_t = None
+    film_t = fx = None
+    xch_ev = []  # (start, end) CUDA events around each timed step's film exchange (RCCL)
     if world > 1:
         import torch
         film_t = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device=coll_dev)
+        fx = FilmExchange(a.width, a.height, rank, world, device=coll_dev if backend == "nccl" else None)
+    timing_xch = [False]
 
     def step():
         rt.clear()
         rt.render(a.spp, tiles=tiles, first_sample=0)
         if world > 1:
             import torch
-            if backend == "nccl":
-                torch.cuda.synchronize()  # the previous step's reduce is done with film_t
-                rt.copy_film_to(film_t.data_ptr())
-                rt.synchronize()  # the copy runs on librtg's stream, the reduce on RCCL's
-            else:
-                film_t.copy_(torch.from_numpy(rt.film()[0]))
-            reduce_film(film_t, dist)
+            ev = None
+            if backend == "nccl" and timing_xch[0]:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            fx.exchange(rt, film_t, dist)  # own tiles -> rank 0 (pack, RCCL gather, scatter)
+            if ev is not None:
+                ev[1].record()
+                xch_ev.append(ev)
 
     def barrier_sync():
         if world > 1:
@@ -277,6 +286,7 @@ def main():
         step()
     # timed region: per-launch HIP events on the render stream give the closest-hit kernel time
     rt.set_options(flags=base | N.RTG_OPT_TIMING)
+    timing_xch[0] = True
     ext_rays = shadow_rays = paths = cam_traced = 0
     extend_ms = shadow_ms = shade_ms = 0.0
     extend_launches = 0
@@ -296,6 +306,15 @@ def main():
         extend_launches += st["extend_launches"]
     barrier_sync()
     elapsed = time.perf_counter() - t_start
+    timing_xch[0] = False
+    xch_ms = [e0.elapsed_time(e1) for e0, e1 in xch_ev]
+
+    # shard-of-N projection: the exchange a rank of N adds to its render, rehearsed on this GPU (the
+    # pack of rank 0's pixels, the scatter rank 0 runs over all N ranks' pixels) plus a model of the
+    # RCCL transfer (rank 0 receives N-1 packed buffers concurrently, one per xGMI link)
+    shard_exchange = None
+    if world == 1 and group_devs is None and a.shard_of > 1:
+        shard_exchange = rehearse_exchange(rt, a)
 
     # the drop-in frame loop (Main.cpp:74-118): one RayTracer::render() = one rtg call of 1 spp
     # (without the per-launch timing events, which keep one chunk in flight)
@@ -351,11 +370,11 @@ def main():
             group_info["rank_render_ms"] = {"max": round(max(rms), 2), "mean": round(float(np.mean(rms)), 2),
                                             "max_over_mean": round(max(rms) / float(np.mean(rms)), 4)}
         if len(set(group_devs)) > 1:
-            group_info["note"] = ("distinct-device group: ranks render concurrently, films reduced by RCCL; "
+            group_info["note"] = ("distinct-device group: ranks render concurrently, own tiles sent to device 0 by RCCL; "
                                   "film_reduce_bit_exact (--verify-film) is its check on this run")
         group_parallelism = ("tile-sharded x%d, one process (rtg_group: a handle and host thread per device) + "
-                             "%s film reduce" % (len(group_devs), "RCCL ncclReduce" if rt.g.uses_rccl
-                                                 else "host-memory (repeated devices)"))
+                             "own-tile film exchange over %s" % (len(group_devs), "RCCL ncclSend/ncclRecv" if rt.g.uses_rccl
+                                                                 else "device copies (repeated devices)"))
         if group_reduced is not None:
             # the group's device memory goes first (ranks rehearsed on one device hold a chunk each)
             del rt
@@ -388,8 +407,15 @@ def main():
      s_nodes, s_tris, c_sh, ext_traced) = totals.tolist()
     rays = ext_rays + shadow_rays
     rays_traced = ext_traced + shadow_rays
-    mrays = rays / t_max / 1e6
+    mrays = rays / t_max / 1e6  # the reference's ray count (a camera ray per sample)
+    mrays_traced = rays_traced / t_max / 1e6
     ms_step = t_max * 1e3 / a.steps
+    if shard_exchange is not None:
+        # the job at N GPUs: every rank renders its share (rank 0's share stands for all: diagonal
+        # stripes are balanced to ~2 %) and rank 0 assembles the film
+        job_ms = ms_step + shard_exchange["total_ms"]
+        shard_exchange["projected_job_ms_per_step"] = round(job_ms, 3)
+        shard_exchange["projected_job_mrays_traced_per_s"] = round(rays_traced * a.shard_of / (job_ms / 1e3 * a.steps) / 1e6, 1)
     if dropin is not None:
         dropin["batched_ms_per_frame"] = round(ms_step / a.spp, 4)
         dropin["queued_over_batched"] = round(dropin["queued"]["ms_per_frame"] / (ms_step / a.spp), 3)
@@ -493,9 +519,9 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": ("Mray/s (closest-hit + shadow rays) at 1024x1024x64spp, synthetic 1M triangles"
-                       if a.config == "C3" else "Mray/s (closest-hit + shadow rays), config %s" % a.config),
-            "value": round(mrays, 2),
+            "metric": ("Mray/s (traced closest-hit + shadow rays) at 1024x1024x64spp, synthetic 1M triangles"
+                       if a.config == "C3" else "Mray/s (traced closest-hit + shadow rays), config %s" % a.config),
+            "value": round(mrays_traced, 2),
             "unit": "Mray/s",
             "n_gpus": world if group_devs is None else len(set(group_devs)),
             **({"ranks": len(group_devs)} if group_devs is not None else {}),
@@ -506,11 +532,13 @@ def main():
             "mpaths_per_s": round(paths / t_max / 1e6, 2),
             "rays_per_path": round(rays / max(paths, 1), 4),
             "rays_traced_per_path": round(rays_traced / max(paths, 1), 4),
-            "mrays_traced_per_s": round(rays_traced / t_max / 1e6, 2),
-            "rays_note": ("value counts the reference's rays: a camera ray per sample, as renderTile casts "
-                          "them (Renderer.h:805-808). That ray is the pixel centre's for every sample, so the "
-                          "traversal traces one per pixel per chunk and the samples share its hit (same film "
-                          "bits); rays_traced_per_path counts the rays traced"),
+            "mrays_traced_per_s": round(mrays_traced, 2),
+            "mrays_reference_equivalent_per_s": round(mrays, 2),
+            "rays_note": ("value counts the rays the traversal traced. renderTile casts the pixel-centre camera "
+                          "ray for every sample (Renderer.h:805-808), so the GPU traces it once per pixel per "
+                          "chunk and the samples share its hit (same film bits); "
+                          "mrays_reference_equivalent_per_s counts it once per sample, as the reference casts "
+                          "it (rays_per_path)"),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -523,7 +551,7 @@ def main():
                            a.width, a.height, a.spp, a.max_depth),
                        "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
                        "max_depth": a.max_depth,
-                       "parallelism": ("tile-sharded x%d + %s film reduce" % (world, "RCCL" if backend == "nccl" else backend)
+                       "parallelism": ("tile-sharded x%d + own-tile film exchange over %s" % (world, "RCCL" if backend == "nccl" else backend)
                                        if group_devs is None else
                                        group_parallelism)},
             # headline roofline: a hardware peak. SURVEY.md 8d's algorithmic bytes of k_trace per
@@ -625,6 +653,12 @@ def main():
             "cpu_baseline": cpu,
             **({"dropin": dropin} if dropin is not None else {}),
             **({"film_reduce_bit_exact": film_check} if film_check is not None else {}),
+            **({"exchange_ms_per_step": {"mean": round(float(np.mean(xch_ms)), 3), "max": round(float(np.max(xch_ms)), 3),
+                                         "bytes_per_rank": fx.maxpix * 12,
+                                         "what": "rank %d: own-tile pack + RCCL gather to rank 0 + scatter (CUDA events "
+                                                 "on the current stream)" % rank}}
+               if xch_ms else {}),
+            **({"shard_exchange": shard_exchange} if shard_exchange is not None else {}),
             **({"group": group_info} if group_info is not None else {}),
             "setup_s": round(setup_s, 2),
         }
@@ -669,7 +703,7 @@ def dropin_leg(rt, a, tiles, base_flags):
             film = rt.film()[0]
             dt = time.perf_counter() - t0
             st = rt.stats()
-            rays = st["extension_rays"] + st["shadow_rays"]
+            rays = st["extension_rays"] - st["paths"] + st["traced_camera_rays"] + st["shadow_rays"]  # traced
             same = same and bool(np.array_equal(film.view(np.uint32), batch_film))
             best = dt if best is None or dt < best else best
         return {"ms_per_frame": round(best * 1e3 / F, 4), "mrays_per_s": round(rays / best / 1e6, 1),
@@ -679,6 +713,48 @@ def dropin_leg(rt, a, tiles, base_flags):
     rt.set_options(flags=base_flags)
     out["batched_ms_per_frame"] = None  # filled by the caller (ms_per_step / spp of the headline)
     return out
+
+
+XGMI_LINK_GBS = 76.5   # one direction of one xGMI link (~153 GB/s per link, both directions): a model
+RCCL_P2P_US = 25.0     # per send/recv round on xGMI, small messages (model)
+
+
+def rehearse_exchange(rt, a, reps=20):
+    """The film exchange a rank of a.shard_of adds to its render, on this GPU: rtg_film_gather of
+    rank 0's own pixels (every rank runs it, concurrently) and rtg_film_scatter of all ranks' pixels
+    into the film (rank 0), timed with CUDA events (median of `reps`); the RCCL transfer between
+    them is modelled: rank 0 receives N-1 buffers of maxpix x 12 B at once, one per xGMI link."""
+    import ctypes as C
+    import torch
+    from raytracingrenderer_amd import _native as N
+    from raytracingrenderer_amd.distributed import FilmExchange
+    n = a.shard_of
+    fx = FilmExchange(a.width, a.height, 0, n, device="cuda:0")
+    film = torch.zeros((a.height, a.width, 3), dtype=torch.float32, device="cuda:0")
+    rt.synchronize()
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def timed(fn):
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return float(np.median(ts))
+    g_ms = timed(lambda: N.rtg().rtg_film_gather(rt.handle, C.c_void_p(fx.t_own.data_ptr()), fx.maxpix,
+                                                   C.c_void_p(fx.recv[0].data_ptr()), stream))
+    s_ms = timed(lambda: N.rtg().rtg_film_scatter(0, C.c_void_p(fx.recv.data_ptr()), C.c_void_p(fx.t_all.data_ptr()),
+                                                    len(fx.all), C.c_void_p(film.data_ptr()), stream))
+    msg = fx.maxpix * 12
+    x_ms = (msg / (XGMI_LINK_GBS * 1e9)) * 1e3 + RCCL_P2P_US / 1e3
+    return {"ranks": n, "bytes_per_rank": msg, "gather_ms": round(g_ms, 4), "scatter_ms": round(s_ms, 4),
+            "xgmi_model_ms": round(x_ms, 4), "total_ms": round(g_ms + s_ms + x_ms, 4),
+            "model": "RCCL transfer modelled as %d B over one xGMI link at %.1f GB/s + %.0f us (rank 0 receives the "
+                     "N-1 buffers on N-1 links at once); gather and scatter measured on this GPU"
+                     % (msg, XGMI_LINK_GBS, RCCL_P2P_US)}
 
 
 def host_cores():

@@ -33,8 +33,10 @@ extern "C" {
 
 /* 2: rtg_scene_desc.projection; 3: rtg_stats.tri_tail_loads / leafbox_tests appended;
  * 4: rtg_render_async queues frames (returns before any of its work has run), rtg_render_idle,
- *    rtg_stats.traced_camera_rays appended */
-#define RTG_ABI_VERSION 4
+ *    rtg_stats.traced_camera_rays appended;
+ * 5: rtg_build_id; the own-tile film exchange (rtg_tile_pixels, rtg_film_gather, rtg_film_scatter),
+ *    which rtg_group_reduce now uses in place of a whole-film ncclReduce */
+#define RTG_ABI_VERSION 5
 
 /* error codes */
 #define RTG_OK              0
@@ -130,6 +132,9 @@ typedef struct rtg_stats {
 typedef struct rtg_handle rtg_handle;
 
 int32_t     rtg_abi_version(void);
+/* Hash of the sources, headers and compile flags this library was built from (build.py
+ * source_hash("device")): a test or smoke run checks it against the tree it runs in. */
+const char* rtg_build_id(void);
 const char* rtg_last_error(void);
 int         rtg_device_count(int* count);
 
@@ -238,13 +243,16 @@ int  rtg_render_adaptive(rtg_handle* h, uint32_t first_sample, uint64_t seed, ui
  * over numProcs CPU threads (Renderer.h:836-853, numProcs from :52-54); here the tiles are spread
  * over devices: rank r of N renders every sample of the tiles with (tile_x + tile_y) % N == r
  * (rtg_tiles_for_rank; the partition of raytracingrenderer_amd/distributed.py), one host thread and
- * one handle per device, and rtg_group_reduce sums the float films into devices[0] with one RCCL
- * ncclReduce (ncclCommInitAll, single process). The reduced film is bit-identical to a one-device
- * render. A device list with repeats (N ranks rehearsed on fewer GPUs) renders the ranks in turn and
- * sums through host memory. The scene's device records are built on the host once and uploaded to
- * the devices in parallel (rtg_group_setup_ms). A failed rtg_group_render leaves the group
- * poisoned (other ranks already added their samples): rtg_group_reduce / film_read return
- * RTG_ERR_ARG until rtg_group_clear. */
+ * one handle per device, and rtg_group_reduce assembles the film on devices[0] from each rank's own
+ * tiles only: every rank packs its tiles' pixels (rtg_film_gather), sends them to devices[0] with
+ * one ncclSend (ncclCommInitAll, single process; devices[0] posts an ncclRecv per rank), and
+ * devices[0] scatters them into the film (rtg_film_scatter). Tile supports are disjoint and cover
+ * the image, so the assembled film is bit-identical to a one-device render (and to the sum of the
+ * films), at 1/N of a whole-film reduce's bytes per rank. A device list with repeats (N ranks
+ * rehearsed on fewer GPUs) renders the ranks in turn and moves the packed tiles with device copies.
+ * The scene's device records are built on the host once and uploaded to the devices in parallel
+ * (rtg_group_setup_ms). A failed rtg_group_render leaves the group poisoned (other ranks already
+ * added their samples): rtg_group_reduce / film_read return RTG_ERR_ARG until rtg_group_clear. */
 typedef struct rtg_group rtg_group;
 int  rtg_tiles_for_rank(uint32_t width, uint32_t height, int rank, int world, uint32_t* tile_ids /* or NULL */,
                         uint32_t* n_tiles);
@@ -254,12 +262,28 @@ int  rtg_group_size(rtg_group* g);
 rtg_handle* rtg_group_handle(rtg_group* g, int rank);  /* e.g. for rtg_get_stats; owned by the group */
 int  rtg_group_set_options(rtg_group* g, int max_depth, int flags, uint32_t max_paths);
 int  rtg_group_render(rtg_group* g, uint32_t first_sample, uint32_t n_samples, uint64_t seed);
-int  rtg_group_reduce(rtg_group* g);  /* the films stay per device; the sum goes to a separate buffer */
+int  rtg_group_reduce(rtg_group* g);  /* the films stay per device; the assembled film goes to a separate buffer */
 int  rtg_group_film_read(rtg_group* g, float* rgb_sum /* width*height*3 */, uint32_t* spp);  /* reduces if needed */
 int  rtg_group_clear(rtg_group* g);
 double rtg_group_reduce_ms(rtg_group* g);  /* device time of the last reduce */
 int  rtg_group_uses_rccl(rtg_group* g);    /* 1: RCCL communicator, 0: host-memory sum (repeated devices) */
 int  rtg_group_setup_ms(rtg_group* g, double* prepare_ms, double* upload_ms);  /* host build, parallel uploads */
+
+/* ---- own-tile film exchange (the data movement of rtg_group_reduce, exposed for hosts that run
+ * one process per GPU, e.g. raytracingrenderer_amd/distributed.py over torch.distributed).
+ * rtg_tile_pixels lists the film pixel indices (y * width + x) of the given 32x32 tiles in the
+ * order rtg_film_gather packs them: tile by tile, row-major inside a tile, clipped at the film
+ * edge (pixels NULL: only the count). rtg_film_gather copies the handle's film pixels listed in
+ * pixels_dev (device array of n indices; 0xFFFFFFFF = padding, packed as zeros) to dst_dev (3n
+ * floats), ordered after every render queued on the handle; rtg_film_scatter writes src_dev's n
+ * packed pixels into film_dev (width * height * 3 floats) at the listed indices (0xFFFFFFFF:
+ * skipped). Both run on hip_stream (NULL: the handle's stream / the device's null stream) and
+ * return without waiting. */
+int  rtg_tile_pixels(uint32_t width, uint32_t height, const uint32_t* tile_ids, uint32_t n_tiles,
+                     uint32_t* pixels /* or NULL */, uint32_t* n_pixels);
+int  rtg_film_gather(rtg_handle* h, const uint32_t* pixels_dev, uint32_t n, float* dst_dev, void* hip_stream);
+int  rtg_film_scatter(int device, const float* src_dev, const uint32_t* pixels_dev, uint32_t n, float* film_dev,
+                      void* hip_stream);
 
 /* Film access: the unnormalised sum (Film::film) and the sample count (Film::SPP). */
 int  rtg_film_read(rtg_handle* h, float* rgb_sum /* width*height*3 */, uint32_t* spp);

@@ -41,6 +41,8 @@ typedef struct rth_scene_info {
 } rth_scene_info;
 
 const char* rth_last_error(void);
+/* Hash of the sources, headers and compile flags this library was built from (build.py). */
+const char* rth_build_id(void);
 
 int  rth_load_scene(const char* scene_dir, const rth_load_options* opts, rth_scene** out);
 void rth_free_scene(rth_scene* s);

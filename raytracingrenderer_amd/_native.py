@@ -74,6 +74,7 @@ class rth_scene_info(C.Structure):
 
 RTG_EXPORTS = [
     ("rtg_abi_version", C.c_int32, []),
+    ("rtg_build_id", C.c_char_p, []),
     ("rtg_last_error", C.c_char_p, []),
     ("rtg_device_count", C.c_int, [i32p]),
     ("rtg_create", C.c_int, [C.c_int, C.POINTER(rtg_scene_desc), C.POINTER(C.c_void_p)]),
@@ -113,10 +114,15 @@ RTG_EXPORTS = [
     ("rtg_group_reduce_ms", C.c_double, [C.c_void_p]),
     ("rtg_group_uses_rccl", C.c_int, [C.c_void_p]),
     ("rtg_group_setup_ms", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    # own-tile film exchange (rtg_multi.hip)
+    ("rtg_tile_pixels", C.c_int, [C.c_uint32, C.c_uint32, u32p, C.c_uint32, u32p, u32p]),
+    ("rtg_film_gather", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("rtg_film_scatter", C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
 ]
 
 RTH_EXPORTS = [
     ("rth_last_error", C.c_char_p, []),
+    ("rth_build_id", C.c_char_p, []),
     ("rth_load_scene", C.c_int, [C.c_char_p, C.POINTER(rth_load_options), C.POINTER(C.c_void_p)]),
     ("rth_free_scene", None, [C.c_void_p]),
     ("rth_scene_desc", C.POINTER(rtg_scene_desc), [C.c_void_p]),

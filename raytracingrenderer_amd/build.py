@@ -9,6 +9,7 @@ Outputs (git-ignored, shipped to the GPU box with the source snapshot):
   oracle/_build/liboracle_rtm.so             test-only CPU restatement, shared math
   oracle/_build/liboracle_libm.so            test-only CPU restatement, C-library math
   oracle/_build/libm_check                   test-only: include/rtg_math.h vs the host glibc
+  oracle/_build/div_rewrites                 test-only: k_shade's reciprocal products vs the divisions
 Every float-producing unit is compiled with -ffp-contract=off (bit-faithful arithmetic).
 """
 import os
@@ -40,6 +41,50 @@ def _newer(out, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+HOST_CXXFLAGS = ["-std=c++17", "-O2", "-ffp-contract=off", "-fPIC", "-shared", "-Wall"]
+DEVICE_CXXFLAGS = ["-O3", "-ffp-contract=off", "-std=c++17", "-fPIC"]
+DEVICE_LDFLAGS = ["-ldl", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
+
+
+def source_hash(which, debug=False):
+    """Build id of a library: sha256 (16 hex digits) over its sources, every header it can include
+    (include/, csrc/<host|device>/*.h) and its compile flags. Embedded in the library
+    (rtg_build_id / rth_build_id); smoke() and the GPU tests check it against the tree they run in,
+    and the build rebuilds whenever the embedded id differs (not by file times)."""
+    import hashlib
+    hsh = hashlib.sha256()
+    if which == "device":
+        src = DEVICE_SRC
+        flags = [ARCH] + DEVICE_CXXFLAGS + DEVICE_LDFLAGS + sum((DEVICE_FLAGS.get(r, []) for r in DEVICE_SRC), [])
+        flags += ["-DRTG_DEBUG=1"] if debug else []
+    else:
+        src = HOST_SRC
+        flags = HOST_CXXFLAGS
+    files = [os.path.join(CSRC, r) for r in src] + sorted(_deps([]))
+    for f in files:
+        hsh.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            hsh.update(fh.read())
+    hsh.update(" ".join(flags).encode())
+    return hsh.hexdigest()[:16]
+
+
+def embedded_id(path, tag):
+    """The build id a built library carries (the `tag` + 16 hex digits string), or None."""
+    try:
+        data = open(path, "rb").read()
+    except OSError:
+        return None
+    i = data.find(tag.encode())
+    if i < 0:
+        return None
+    return data[i + len(tag):i + len(tag) + 16].decode("ascii", "replace")
+
+
+def _stale(out, which, tag, debug=False):
+    return not os.path.exists(out) or embedded_id(out, tag) != source_hash(which, debug)
+
+
 def _deps(paths):
     extra = [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
     for sub in ("host", "device"):
@@ -60,9 +105,9 @@ def build_host(force=False):
     os.makedirs(LIB, exist_ok=True)
     out = os.path.join(LIB, "librth.so")
     src = [os.path.join(CSRC, s) for s in HOST_SRC]
-    if force or _newer(out, _deps(src)):
-        _run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fPIC", "-shared", "-Wall",
-              "-o", out] + src + ["-lz", "-lpthread"])
+    if force or _stale(out, "host", "rth-build-id:"):
+        _run(["g++"] + HOST_CXXFLAGS + ['-DRTH_BUILD_ID="%s"' % source_hash("host"), "-o", out] + src +
+             ["-lz", "-lpthread"])
     return out
 
 
@@ -71,13 +116,14 @@ def build_device(force=False, debug=False):
     os.makedirs(d, exist_ok=True)
     out = os.path.join(d, "librtg.so")
     src = [os.path.join(CSRC, s) for s in DEVICE_SRC]
-    if force or _newer(out, _deps(src)):
+    if force or _stale(out, "device", "rtg-build-id:", debug):
+        bid = source_hash("device", debug)
         # one object per unit (each with its own flags, compiled in parallel), then one link
         with tempfile.TemporaryDirectory() as tmp:
             objs, procs = [], []
             for rel, path in zip(DEVICE_SRC, src):
                 obj = os.path.join(tmp, os.path.basename(rel) + ".o")
-                cmd = ([HIPCC, "--offload-arch=" + ARCH, "-O3", "-ffp-contract=off", "-std=c++17", "-fPIC"] +
+                cmd = ([HIPCC, "--offload-arch=" + ARCH] + DEVICE_CXXFLAGS + ['-DRTG_BUILD_ID="%s"' % bid] +
                        (["-DRTG_DEBUG=1"] if debug else []) + DEVICE_FLAGS.get(rel, []) + ["-c", "-o", obj, path])
                 procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
                 objs.append(obj)
@@ -86,8 +132,7 @@ def build_device(force=False, debug=False):
                 if pr.returncode != 0:
                     sys.stderr.write(log)
                     raise RuntimeError("build failed: " + " ".join(cmd))
-            _run([HIPCC, "--offload-arch=" + ARCH, "-fPIC", "-shared", "-o", out] + objs +
-                 ["-ldl", "-Wl,-rpath,/opt/rocm/lib"])
+            _run([HIPCC, "--offload-arch=" + ARCH, "-fPIC", "-shared", "-o", out] + objs + DEVICE_LDFLAGS)
     return out
 
 
@@ -118,7 +163,36 @@ def build_oracle(force=False):
     if force or _newer(chk, _deps([chk_src])):
         _run(["gcc", "-std=c11", "-O2", "-ffp-contract=off", "-fno-builtin", "-pthread", "-o", chk, chk_src, "-lm"])
     outs.append(chk)
+    # the divisions by pi that k_shade computes as products with a reciprocal, checked exhaustively
+    dv = os.path.join(ORACLE_BUILD, "div_rewrites")
+    dv_src = os.path.join(ORACLE, "div_rewrites.c")
+    if force or _newer(dv, [dv_src]):
+        _run(["gcc", "-std=c11", "-O2", "-ffp-contract=off", "-D_GNU_SOURCE", "-pthread", "-o", dv, dv_src, "-lm"])
+    outs.append(dv)
     return outs
+
+
+SAN_FLAGS = ["-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
+             "-ffp-contract=off"]
+
+
+def build_sanitized(force=False):
+    """Test infrastructure: the host front-end's sources (librth) and the C oracle built with
+    AddressSanitizer + UBSan into one driver, tests/native/_build/host_sanitize
+    (tests/native/host_sanitize.cpp: scenes, textures and corrupted copies of every input file;
+    tests/test_sanitize.py runs it). CPU only; nothing on the GPU is sanitized."""
+    nat = os.path.join(ROOT, "tests", "native")
+    out_dir = os.path.join(nat, "_build")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "host_sanitize")
+    drv = os.path.join(nat, "host_sanitize.cpp")
+    orc = os.path.join(ORACLE, "rt_oracle.c")
+    src = [os.path.join(CSRC, s) for s in HOST_SRC]
+    if force or _newer(out, _deps(src + [drv, orc])):
+        obj = os.path.join(out_dir, "rt_oracle_san.o")
+        _run(["gcc", "-std=c11", "-D_GNU_SOURCE", "-DORACLE_LIBM=0", "-c", "-o", obj, orc] + SAN_FLAGS)
+        _run(["g++", "-std=c++17", "-o", out, drv] + src + [obj] + SAN_FLAGS + ["-lz", "-lpthread", "-lm"])
+    return out
 
 
 def build_ref(force=False):

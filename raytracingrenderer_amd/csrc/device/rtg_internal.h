@@ -7,6 +7,7 @@
 #include "../../../include/rtg.h"
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <string>
 #include <vector>
@@ -193,6 +194,18 @@ static __device__ __forceinline__ unsigned prefix_lt(unsigned long long m) {
 
 // ------------------------------------------------------------------ host side
 extern thread_local std::string g_err;
+
+// roctx ranges around the host-side stages of a render (generate / trace(b) /
+// shade(b) / accumulate); rocprofv3 --marker-trace shows them beside the kernel trace. A range
+// spans the enqueue of its launches (the kernels themselves are in the kernel trace).
+struct RoctxRange {
+    explicit RoctxRange(const char* m) { roctxRangePushA(m); }
+    ~RoctxRange() { roctxRangePop(); }
+    RoctxRange(const RoctxRange&) = delete;
+    RoctxRange& operator=(const RoctxRange&) = delete;
+};
+// "rtg:trace b=<b>" / "rtg:shade b=<b>" names for b < 32 (static strings: roctx copies nothing)
+const char* roctx_stage_name(int kind, int b);
 
 #define HIPOK(expr)                                                                          \
     do {                                                                                     \

@@ -870,8 +870,13 @@ int flush_pending(rtg_handle* h) {
     h->pend_n = 0;
     const bool all = h->pend_key.size() == 1 && h->pend_key[0] == 0xffffffffu;
     const std::vector<uint32_t> key = h->pend_key;
-    return render_impl(h, first, n, h->pend_seed, all ? nullptr : key.data(), all ? 0u : (uint32_t)key.size(),
-                       h->stream, true, false);
+    const int rc = render_impl(h, first, n, h->pend_seed, all ? nullptr : key.data(), all ? 0u : (uint32_t)key.size(),
+                               h->stream, true, false);
+    // rtg_render_async counted the frames in Film::SPP when they were queued; frames whose issue
+    // failed never reach the film (chunks issued before the failure may have: the film is then
+    // partial, and the error says so)
+    if (rc) h->spp -= std::min(h->spp, n);
+    return rc;
 }
 
 int join_frames(rtg_handle* h) {
@@ -1069,6 +1074,13 @@ static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& l
 extern "C" {
 
 int32_t rtg_abi_version(void) { return RTG_ABI_VERSION; }
+#ifndef RTG_BUILD_ID
+#define RTG_BUILD_ID "unknown"
+#endif
+// build.py passes the hash of the sources, headers and flags (source_hash("device")); the tagged
+// copy lets the build find the id in the file without loading it
+static const char k_build_tag[] __attribute__((used)) = "rtg-build-id:" RTG_BUILD_ID;
+const char* rtg_build_id(void) { return k_build_tag + 13; }
 const char* rtg_last_error(void) { return g_err.c_str(); }
 
 int rtg_device_count(int* count) {
@@ -1611,8 +1623,28 @@ static void print_wavetime(const std::vector<unsigned long long>& wt, int maxb, 
     }
 }
 
+const char* roctx_stage_name(int kind, int b) {
+    static const char* const trace[32] = {
+        "rtg:trace b=0", "rtg:trace b=1", "rtg:trace b=2", "rtg:trace b=3", "rtg:trace b=4", "rtg:trace b=5",
+        "rtg:trace b=6", "rtg:trace b=7", "rtg:trace b=8", "rtg:trace b=9", "rtg:trace b=10", "rtg:trace b=11",
+        "rtg:trace b=12", "rtg:trace b=13", "rtg:trace b=14", "rtg:trace b=15", "rtg:trace b=16", "rtg:trace b=17",
+        "rtg:trace b=18", "rtg:trace b=19", "rtg:trace b=20", "rtg:trace b=21", "rtg:trace b=22", "rtg:trace b=23",
+        "rtg:trace b=24", "rtg:trace b=25", "rtg:trace b=26", "rtg:trace b=27", "rtg:trace b=28", "rtg:trace b=29",
+        "rtg:trace b=30", "rtg:trace b=31"};
+    static const char* const shade[32] = {
+        "rtg:shade b=0", "rtg:shade b=1", "rtg:shade b=2", "rtg:shade b=3", "rtg:shade b=4", "rtg:shade b=5",
+        "rtg:shade b=6", "rtg:shade b=7", "rtg:shade b=8", "rtg:shade b=9", "rtg:shade b=10", "rtg:shade b=11",
+        "rtg:shade b=12", "rtg:shade b=13", "rtg:shade b=14", "rtg:shade b=15", "rtg:shade b=16", "rtg:shade b=17",
+        "rtg:shade b=18", "rtg:shade b=19", "rtg:shade b=20", "rtg:shade b=21", "rtg:shade b=22", "rtg:shade b=23",
+        "rtg:shade b=24", "rtg:shade b=25", "rtg:shade b=26", "rtg:shade b=27", "rtg:shade b=28", "rtg:shade b=29",
+        "rtg:shade b=30", "rtg:shade b=31"};
+    if (b < 0 || b >= 32) return kind ? "rtg:shade" : "rtg:trace";
+    return kind ? shade[b] : trace[b];
+}
+
 int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed,
                        const uint32_t* tiles, uint32_t n_tiles, hipStream_t st, bool lazy, bool add_spp) {
+    RoctxRange r_render(lazy ? "rtg:render (queued chunks)" : "rtg:render");
     int rc = set_pixels(h, tiles, n_tiles);
     if (rc) return rc;
     if (h->npix == 0 || n_samples == 0) return RTG_OK;
@@ -1722,13 +1754,17 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         if (hostgrid && !h->cstream) HIPOK(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
         HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), ss));
         timed_begin(h, ss, k);
-        hipLaunchKernelGGL(k_generate, dim3((a.npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, ss, a, pb);  // lean: per pixel
-        LAUNCH_OK("k_generate");
+        {
+            RoctxRange r_gen("rtg:generate");
+            hipLaunchKernelGGL(k_generate, dim3((a.npix + RTG_TB - 1) / RTG_TB), dim3(RTG_TB), 0, ss, a, pb);  // lean: per pixel
+            LAUNCH_OK("k_generate");
+        }
         timed_end(h, ss, k); kinds.push_back(2); ++k;
         // Trace launch L_b (b = 0..maxb) carries the extension rays of bounce b (from shade(b-1),
         // or generate) and the shadow rays of bounce b-1: one persistent launch, one drain tail.
         for (int b = 0; b <= maxb; ++b) {
             if (b > 0) {
+                RoctxRange r_shade(roctx_stage_name(1, b - 1));
                 // one 256-path tile per block: 8 x the largest segment's live tiles (the segment
                 // counts of bounce b - 1 arrived while k_trace(b - 1) ran; bounce 0: the camera rays)
                 unsigned tiles = hostgrid ? 0u : a.seg_tiles;
@@ -1802,12 +1838,16 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                 io.cap_n = (unsigned)cn;
             }
             timed_begin(h, ss, k);
-            if ((rc = launch_trace(h, io, ss))) return rc;
+            {
+                RoctxRange r_trace(roctx_stage_name(0, b));
+                if ((rc = launch_trace(h, io, ss))) return rc;
+            }
             timed_end(h, ss, k); kinds.push_back(0); ++k;
         }
         hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, ss, pb.ctr, maxb, h->d_stats);
         LAUNCH_OK("k_tally");
         // the film takes the chunks in sample order: this fold runs after the previous chunk's
+        RoctxRange r_acc("rtg:accumulate");
         if (h->last_fold) HIPOK(hipStreamWaitEvent(ss, h->last_fold, 0));
         timed_begin(h, ss, k);
         if (a.ns > 1) {
@@ -1835,8 +1875,11 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     }
     if (add_spp) h->spp += n_samples;
     if (lazy) return RTG_OK;
-    // the caller's stream waits for the chunks (and for every chunk queued before them)
-    h->inflight = false;
+    // the caller's stream waits for the chunks (and for every chunk queued before them). The queued
+    // chunks are joined to the handle's own stream only when that is the caller's stream; a render
+    // on a user stream leaves them in flight, so join_frames (film read, clear, stats) still makes
+    // the handle's stream wait for them
+    if (st == h->stream) h->inflight = false;
     HIPOK(hipStreamWaitEvent(st, h->last_fold, 0));
     HIPOK(hipEventRecord(h->ev[1], st));
     if (h->timing) {
@@ -1882,8 +1925,9 @@ int rtg_render_async(rtg_handle* h, uint32_t first, uint32_t n, uint64_t seed, c
         h->pend_seed = seed;
         h->pend_key.swap(key);
     }
+    if (h->npix == 0) return RTG_OK;  // no pixels: nothing is rendered and Film::SPP stays (as rtg_render)
     h->pend_n += n;
-    h->spp += n;  // Film::SPP counts the queued frames at once
+    h->spp += n;  // Film::SPP counts the queued frames at once (taken back if their issue fails)
     if (h->no_coalesce || (uint64_t)h->pend_n * h->npix >= RTG_COALESCE_P) return flush_pending(h);
     return RTG_OK;
 }

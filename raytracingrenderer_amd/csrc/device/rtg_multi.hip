@@ -1,18 +1,23 @@
-// rtg_multi.hip — one-node multi-GPU rendering behind the C-ABI (include/rtg.h, rtg_group_*).
+// rtg_multi.hip — one-node multi-GPU rendering behind the C-ABI (include/rtg.h, rtg_group_*), and
+// the own-tile film exchange (rtg_tile_pixels / rtg_film_gather / rtg_film_scatter).
 //
 // RTBase's only parallelism is the tile pool of RayTracer::pathTracerTileBased (Renderer.h:836-853:
 // numProcs threads pop 32x32 tiles from a shared queue, Renderer.h:52-54). Here the tiles are
 // spread over the GPUs of one node instead: device r renders every sample of the tiles with
 // (tile_x + tile_y) % N == r (diagonal stripes, the same partition as raytracingrenderer_amd/
-// distributed.py), one host thread and one rtg_handle per device, and the float films are summed
-// into the first device with one RCCL reduce over xGMI (ncclCommInitAll over the devices, single
-// process). Tile supports are disjoint and every other device adds +0.0, so the reduced film is
-// bit-identical to a one-GPU render, whatever the reduction order.
+// distributed.py), one host thread and one rtg_handle per device. The film is then assembled on
+// the first device from each rank's own tiles: rank r packs the pixels of its tiles (k_film_gather,
+// 12 B per pixel: 1/N of the film), sends them with one ncclSend over xGMI (ncclCommInitAll over
+// the devices, single process; the first device posts one ncclRecv per rank inside the same RCCL
+// group), and the first device scatters every rank's pixels into the film (k_film_scatter). Tile
+// supports are disjoint and cover the image, so the assembled film is the one-GPU film bit for
+// bit. (Until round 4 every rank sent its whole film to an ncclReduce: N x the bytes, 7/8 of them
+// +0.0 at N = 8.)
 //
 // A device list that repeats a device (rehearsing N ranks on one GPU) cannot form an RCCL
 // communicator; the ranks then render one after another, each with an equal share of the device's
-// memory for its chunks (rtg_handle::mem_cap), and the films are summed through host memory in
-// rank order (same bits).
+// memory for its chunks (rtg_handle::mem_cap), and the packed tiles move with device copies into
+// the same receive buffer and scatter as the RCCL path.
 //
 // Setup: the scene's device records are built once on the host (prepare_scene: triangle records,
 // the wide tree over the reference leaves, leaf boxes, materials, textures) and uploaded to every
@@ -41,7 +46,8 @@ struct Rccl {
     bool tried = false, ok = false;
     ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
-    ncclResult_t (*reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*group_start)() = nullptr;
     ncclResult_t (*group_end)() = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
@@ -61,11 +67,12 @@ bool load_rccl() {
     }
     g_rccl.comm_init_all = (decltype(g_rccl.comm_init_all))dlsym(h, "ncclCommInitAll");
     g_rccl.comm_destroy = (decltype(g_rccl.comm_destroy))dlsym(h, "ncclCommDestroy");
-    g_rccl.reduce = (decltype(g_rccl.reduce))dlsym(h, "ncclReduce");
+    g_rccl.send = (decltype(g_rccl.send))dlsym(h, "ncclSend");
+    g_rccl.recv = (decltype(g_rccl.recv))dlsym(h, "ncclRecv");
     g_rccl.group_start = (decltype(g_rccl.group_start))dlsym(h, "ncclGroupStart");
     g_rccl.group_end = (decltype(g_rccl.group_end))dlsym(h, "ncclGroupEnd");
     g_rccl.error_string = (decltype(g_rccl.error_string))dlsym(h, "ncclGetErrorString");
-    g_rccl.ok = g_rccl.comm_init_all && g_rccl.comm_destroy && g_rccl.reduce && g_rccl.group_start &&
+    g_rccl.ok = g_rccl.comm_init_all && g_rccl.comm_destroy && g_rccl.send && g_rccl.recv && g_rccl.group_start &&
                 g_rccl.group_end && g_rccl.error_string;
     if (!g_rccl.ok) g_err = "RCCL: missing symbols";
     return g_rccl.ok;
@@ -81,12 +88,61 @@ struct EventPair {
 };
 }  // namespace
 
+// Own-tile film exchange. Pack: dst[i] = film[pix[i]] (3 floats; a padding index packs zeros).
+// Scatter: film[pix[i]] = src[i] (padding skipped). One thread per pixel, 12-B reads and writes:
+// HBM-bound, 24 B per pixel moved.
+#define RTG_PIX_PAD 0xFFFFFFFFu
+__global__ __launch_bounds__(256) void k_film_gather(const float* __restrict__ film, const uint32_t* __restrict__ pix,
+                                                     uint32_t n, float* __restrict__ dst) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t p = pix[i];
+    float r = 0.0f, g = 0.0f, b = 0.0f;
+    if (p != RTG_PIX_PAD) {
+        r = film[3 * (size_t)p];
+        g = film[3 * (size_t)p + 1];
+        b = film[3 * (size_t)p + 2];
+    }
+    dst[3 * (size_t)i] = r;
+    dst[3 * (size_t)i + 1] = g;
+    dst[3 * (size_t)i + 2] = b;
+}
+
+__global__ __launch_bounds__(256) void k_film_scatter(const float* __restrict__ src, const uint32_t* __restrict__ pix,
+                                                      uint32_t n, float* __restrict__ film) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t p = pix[i];
+    if (p == RTG_PIX_PAD) return;
+    film[3 * (size_t)p] = src[3 * (size_t)i];
+    film[3 * (size_t)p + 1] = src[3 * (size_t)i + 1];
+    film[3 * (size_t)p + 2] = src[3 * (size_t)i + 2];
+}
+
+// the pixel order of set_pixels (rtg_kernels.hip): tile by tile, row-major inside a tile
+static void tile_pixels(uint32_t W, uint32_t H, const uint32_t* tiles, uint32_t n_tiles, std::vector<uint32_t>& out) {
+    const uint32_t tx = (W + 31) / 32;
+    for (uint32_t i = 0; i < n_tiles; ++i) {
+        const uint32_t bx = (tiles[i] % tx) * 32, by = (tiles[i] / tx) * 32;
+        for (uint32_t y = by; y < std::min<uint32_t>(by + 32, H); ++y)
+            for (uint32_t x = bx; x < std::min<uint32_t>(bx + 32, W); ++x) out.push_back(y * W + x);
+    }
+}
+
 struct rtg_group {
     std::vector<int> devices;
     std::vector<rtg_handle*> h;
     std::vector<std::vector<uint32_t>> tiles;  // per rank
-    std::vector<ncclComm_t> comms;             // empty: host reduce (repeated devices)
-    float* d_sum = nullptr;                    // reduced film on devices[0]
+    std::vector<ncclComm_t> comms;             // empty: device copies (repeated devices)
+    float* d_sum = nullptr;                    // assembled film on devices[0]
+    // own-tile exchange: rank r's pixel list and pack buffer on its device (npix[r] pixels); on
+    // devices[0] the receive buffer (rank r's pixels at r * maxpix) and the matching pixel lists
+    std::vector<uint32_t*> d_pix;
+    std::vector<float*> d_pack;
+    std::vector<uint32_t> npix;
+    uint32_t maxpix = 0;
+    uint32_t* d_pix_all = nullptr;
+    float* d_recv = nullptr;
     uint32_t W = 0, H = 0;
     uint32_t reduced_spp = 0;
     bool reduced = false;
@@ -96,7 +152,88 @@ struct rtg_group {
     double prepare_ms = 0.0, upload_ms = 0.0;  // group setup: host build once, parallel uploads
 };
 
+// the own-tile exchange's buffers: per rank its pixel list + pack buffer on its device, on devices[0]
+// a receive buffer of N x maxpix pixels and the concatenated (padded) pixel lists
+static int exchange_setup(rtg_group* g) {
+    const size_t n = g->h.size();
+    std::vector<std::vector<uint32_t>> pl(n);
+    for (size_t r = 0; r < n; ++r) {
+        tile_pixels(g->W, g->H, g->tiles[r].data(), (uint32_t)g->tiles[r].size(), pl[r]);
+        g->npix.push_back((uint32_t)pl[r].size());
+        g->maxpix = std::max(g->maxpix, (uint32_t)pl[r].size());
+    }
+    const size_t mp = std::max<uint32_t>(g->maxpix, 1);
+    std::vector<uint32_t> all(n * mp, RTG_PIX_PAD);
+    for (size_t r = 0; r < n; ++r) std::copy(pl[r].begin(), pl[r].end(), all.begin() + r * mp);
+    HIPOK(hipSetDevice(g->devices[0]));
+    HIPOK(hipMalloc((void**)&g->d_recv, n * mp * 3 * sizeof(float)));
+    if (dev_upload(&g->d_pix_all, all)) return RTG_ERR_HIP;
+    g->d_pix.assign(n, nullptr);
+    g->d_pack.assign(n, nullptr);
+    for (size_t r = 0; r < n; ++r) {
+        HIPOK(hipSetDevice(g->devices[r]));
+        if (dev_upload(&g->d_pix[r], pl[r])) return RTG_ERR_HIP;
+        if (r == 0) g->d_pack[r] = g->d_recv;
+        else HIPOK(hipMalloc((void**)&g->d_pack[r], mp * 3 * sizeof(float)));
+    }
+    return RTG_OK;
+}
+
 extern "C" {
+
+int rtg_tile_pixels(uint32_t width, uint32_t height, const uint32_t* tile_ids, uint32_t n_tiles, uint32_t* pixels,
+                    uint32_t* n_pixels) {
+    if (!n_pixels || (!tile_ids && n_tiles)) {
+        g_err = "rtg_tile_pixels: bad argument";
+        return RTG_ERR_ARG;
+    }
+    const uint32_t nt = ((width + 31) / 32) * ((height + 31) / 32);
+    for (uint32_t i = 0; i < n_tiles; ++i)
+        if (tile_ids[i] >= nt) {
+            g_err = "rtg_tile_pixels: tile id out of range";
+            return RTG_ERR_ARG;
+        }
+    std::vector<uint32_t> pl;
+    tile_pixels(width, height, tile_ids, n_tiles, pl);
+    *n_pixels = (uint32_t)pl.size();
+    if (pixels) std::copy(pl.begin(), pl.end(), pixels);
+    return RTG_OK;
+}
+
+int rtg_film_gather(rtg_handle* h, const uint32_t* pixels_dev, uint32_t n, float* dst_dev, void* stream) {
+    if (!h || (n && (!pixels_dev || !dst_dev))) {
+        g_err = "rtg_film_gather: bad argument";
+        return RTG_ERR_ARG;
+    }
+    HIPOK(hipSetDevice(h->device));
+    if (int rc = join_frames(h)) return rc;  // the film holds every queued frame first
+    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    if (st != h->stream) {
+        HIPOK(hipEventRecord(h->ev[2], h->stream));
+        HIPOK(hipStreamWaitEvent(st, h->ev[2], 0));
+    }
+    if (n) {
+        hipLaunchKernelGGL(k_film_gather, dim3((n + 255) / 256), dim3(256), 0, st, (const float*)h->d_film, pixels_dev, n,
+                           dst_dev);
+        LAUNCH_OK("k_film_gather");
+    }
+    return RTG_OK;
+}
+
+int rtg_film_scatter(int device, const float* src_dev, const uint32_t* pixels_dev, uint32_t n, float* film_dev,
+                     void* stream) {
+    if (n && (!src_dev || !pixels_dev || !film_dev)) {
+        g_err = "rtg_film_scatter: bad argument";
+        return RTG_ERR_ARG;
+    }
+    HIPOK(hipSetDevice(device));
+    if (n) {
+        hipLaunchKernelGGL(k_film_scatter, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, src_dev, pixels_dev,
+                           n, film_dev);
+        LAUNCH_OK("k_film_scatter");
+    }
+    return RTG_OK;
+}
 
 int rtg_tiles_for_rank(uint32_t width, uint32_t height, int rank, int world, uint32_t* tile_ids, uint32_t* n_tiles) {
     if (!n_tiles || world < 1 || rank < 0 || rank >= world) {
@@ -117,9 +254,16 @@ int rtg_tiles_for_rank(uint32_t width, uint32_t height, int rank, int world, uin
 void rtg_group_destroy(rtg_group* g) {
     if (!g) return;
     for (ncclComm_t c : g->comms) (void)g_rccl.comm_destroy(c);
-    if (g->d_sum) {
+    for (size_t r = 0; r < g->d_pix.size(); ++r) {
+        (void)hipSetDevice(g->devices[r]);
+        (void)hipFree(g->d_pix[r]);
+        if (r > 0) (void)hipFree(g->d_pack[r]);  // rank 0 packs straight into d_recv
+    }
+    if (!g->devices.empty()) {
         (void)hipSetDevice(g->devices[0]);
         (void)hipFree(g->d_sum);
+        (void)hipFree(g->d_recv);
+        (void)hipFree(g->d_pix_all);
     }
     for (rtg_handle* h : g->h) rtg_destroy(h);
     delete g;
@@ -209,6 +353,10 @@ int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* de
         rtg_group_destroy(g);
         return RTG_ERR_HIP;
     }
+    if (int rc2 = exchange_setup(g)) {
+        rtg_group_destroy(g);
+        return rc2;
+    }
     *out = g;
     return RTG_OK;
 }
@@ -270,49 +418,53 @@ int rtg_group_reduce(rtg_group* g) {
         return RTG_ERR_ARG;
     }
     const size_t n = g->h.size();
-    const size_t count = (size_t)g->W * g->H * 3;
+    const size_t mp = std::max<uint32_t>(g->maxpix, 1);
     EventPair ev;
     HIPOK(hipSetDevice(g->devices[0]));
     HIPOK(hipEventCreate(&ev.e0));
     HIPOK(hipEventCreate(&ev.e1));
     HIPOK(hipEventRecord(ev.e0, g->h[0]->stream));
+    // every rank packs its own tiles' pixels on its device (rank 0 straight into the receive buffer)
+    for (size_t r = 0; r < n; ++r)
+        if (int rc = rtg_film_gather(g->h[r], g->d_pix[r], g->npix[r], g->d_pack[r], nullptr)) return rc;
     if (!g->comms.empty()) {
-        // every rank's film (summed in sample order on its device) -> device 0, ncclSum. Every
-        // failure inside the group still closes it (ncclGroupEnd), so the thread's RCCL group
-        // state stays balanced.
+        // one ncclSend per rank > 0 to device 0, which posts the matching ncclRecv into slot r of its
+        // receive buffer. Every failure inside the group still closes it (ncclGroupEnd), so the
+        // thread's RCCL group state stays balanced.
         if (g_rccl.group_start() != ncclSuccess) { g_err = "ncclGroupStart failed"; return RTG_ERR_HIP; }
         std::string fail;
-        for (size_t r = 0; r < n && fail.empty(); ++r) {
-            const hipError_t he = hipSetDevice(g->devices[r]);
-            if (he != hipSuccess) {
-                fail = std::string("hipSetDevice: ") + hipGetErrorString(he);
-                break;
-            }
-            const ncclResult_t nr = g_rccl.reduce(g->h[r]->d_film, r == 0 ? g->d_sum : nullptr, count, ncclFloat, ncclSum,
-                                                  0, g->comms[r], g->h[r]->stream);
-            if (nr != ncclSuccess) fail = std::string("ncclReduce: ") + g_rccl.error_string(nr);
+        for (size_t r = 1; r < n && fail.empty(); ++r) {
+            if (!g->npix[r]) continue;
+            const size_t cnt = (size_t)g->npix[r] * 3;
+            ncclResult_t nr = g_rccl.send(g->d_pack[r], cnt, ncclFloat, 0, g->comms[r], g->h[r]->stream);
+            if (nr == ncclSuccess)
+                nr = g_rccl.recv(g->d_recv + r * mp * 3, cnt, ncclFloat, (int)r, g->comms[0], g->h[0]->stream);
+            if (nr != ncclSuccess) fail = std::string("ncclSend/ncclRecv: ") + g_rccl.error_string(nr);
         }
         const ncclResult_t nr = g_rccl.group_end();
         if (!fail.empty()) { g_err = fail; return RTG_ERR_HIP; }
         if (nr != ncclSuccess) { g_err = std::string("ncclGroupEnd: ") + g_rccl.error_string(nr); return RTG_ERR_HIP; }
-        for (size_t r = 0; r < n; ++r) {
+    } else {
+        // repeated devices: the packed tiles move with device copies, in rank order
+        for (size_t r = 1; r < n; ++r) {
+            if (!g->npix[r]) continue;
             HIPOK(hipSetDevice(g->devices[r]));
             HIPOK(hipStreamSynchronize(g->h[r]->stream));
+            HIPOK(hipSetDevice(g->devices[0]));
+            HIPOK(hipMemcpyPeerAsync(g->d_recv + r * mp * 3, g->devices[0], g->d_pack[r], g->devices[r],
+                                     (size_t)g->npix[r] * 3 * sizeof(float), g->h[0]->stream));
         }
-    } else {
-        // repeated devices: rank order through host memory
-        std::vector<float> sum(count, 0.0f), f(count);
-        for (size_t r = 0; r < n; ++r) {
-            uint32_t spp = 0;
-            const int rc = rtg_film_read(g->h[r], f.data(), &spp);
-            if (rc) return rc;
-            for (size_t i = 0; i < count; ++i) sum[i] = sum[i] + f[i];
-        }
-        HIPOK(hipSetDevice(g->devices[0]));
-        HIPOK(hipMemcpy(g->d_sum, sum.data(), count * sizeof(float), hipMemcpyHostToDevice));
     }
     HIPOK(hipSetDevice(g->devices[0]));
+    HIPOK(hipMemsetAsync(g->d_sum, 0, (size_t)g->W * g->H * 3 * sizeof(float), g->h[0]->stream));
+    if (int rc = rtg_film_scatter(g->devices[0], g->d_recv, g->d_pix_all, (uint32_t)(n * mp), g->d_sum, g->h[0]->stream))
+        return rc;
     HIPOK(hipEventRecord(ev.e1, g->h[0]->stream));
+    for (size_t r = 1; r < n && !g->comms.empty(); ++r) {
+        HIPOK(hipSetDevice(g->devices[r]));
+        HIPOK(hipStreamSynchronize(g->h[r]->stream));
+    }
+    HIPOK(hipSetDevice(g->devices[0]));
     HIPOK(hipEventSynchronize(ev.e1));
     float ms = 0.0f;
     (void)hipEventElapsedTime(&ms, ev.e0, ev.e1);

@@ -87,7 +87,13 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             h = p.hits[j];
             if (h.x < RTG_FLT_MAX) S = s.shade[__float_as_int(h.y)];
         }
-        if (TAB) __syncthreads();  // (waits for the table loads: vmcnt(0))
+        if (TAB) {
+            // global_load_lds completes on vmcnt, not on the barrier: wait for it explicitly (the
+            // payload loads above are then in too) before other waves read the tables.
+            // tests/test_kernel_resources.py pins the s_waitcnt vmcnt(0) ahead of this s_barrier
+            __builtin_amdgcn_s_waitcnt(0);
+            __syncthreads();
+        }
         if (valid) {
             pid = lean0 ? (int)i : __float_as_int(ro.w);  // the path id travels in ray_o.w
             const v3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);

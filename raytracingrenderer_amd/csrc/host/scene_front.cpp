@@ -505,6 +505,13 @@ extern "C" {
 
 const char* rth_last_error(void) { return g_err.c_str(); }
 
+#ifndef RTH_BUILD_ID
+#define RTH_BUILD_ID "unknown"
+#endif
+// build.py passes the hash of the sources, headers and flags (source_hash("host"))
+static const char k_build_tag[] __attribute__((used)) = "rth-build-id:" RTH_BUILD_ID;
+const char* rth_build_id(void) { return k_build_tag + 13; }
+
 int rth_load_scene(const char* scene_dir, const rth_load_options* opts, rth_scene** out) {
     if (!scene_dir || !out) { g_err = "rth_load_scene: null argument"; return RTG_ERR_ARG; }
     rth_load_options o{};

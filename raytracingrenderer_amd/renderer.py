@@ -203,6 +203,11 @@ class RayTracer:
         _check(self._lib.rtg_set_options(self._h, self.max_depth, self.flags, max_paths), self._lib.rtg_last_error)
 
     @property
+    def handle(self):
+        """The rtg_handle* (ctypes void pointer) for direct C-ABI calls (e.g. rtg_film_gather)."""
+        return self._h
+
+    @property
     def tiles_x(self):
         return (self.width + 31) // 32
 
@@ -315,10 +320,11 @@ class RayTracer:
 class RayTracerGroup:
     """RayTracer over several GPUs of one node (rtg_group_*, rtg_multi.hip): rank r renders the 32x32
     tiles with (tile_x + tile_y) % N == r on devices[r] (one host thread per device), and film()
-    sums the films into devices[0] with one RCCL reduce. The result is bit-identical to a one-device
-    render (RayTracer::pathTracerTileBased's tile pool, Renderer.h:836-853, spread over devices).
-    A device list with repeats rehearses N ranks on fewer GPUs (the ranks then render in turn and
-    the sum goes through host memory)."""
+    assembles the film on devices[0] from every rank's own tiles (packed on each device, one RCCL
+    send per rank, scattered on devices[0]). The result is bit-identical to a one-device render
+    (RayTracer::pathTracerTileBased's tile pool, Renderer.h:836-853, spread over devices). A device
+    list with repeats rehearses N ranks on fewer GPUs (the ranks then render in turn and the packed
+    tiles move with device copies)."""
 
     def __init__(self, scene, devices=(0,), max_depth=RayTracer.MAX_DEPTH, seed=1234, cull=True, max_paths=0):
         self.scene = scene
@@ -351,7 +357,8 @@ class RayTracerGroup:
         return a.value, b.value
 
     def reduce(self):
-        """The RCCL film reduce into devices[0] (host sum for repeated devices); synchronous."""
+        """Assemble the film on devices[0] from every rank's own tiles (RCCL send/recv; device copies
+        for repeated devices); synchronous."""
         _check(self._lib.rtg_group_reduce(self._g), self._lib.rtg_last_error)
 
     def rank_stats(self):

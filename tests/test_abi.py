@@ -31,7 +31,34 @@ def test_exports_cover_header(header, lib):
 
 
 def test_abi_version():
-    assert N.rtg().rtg_abi_version() == 4
+    assert N.rtg().rtg_abi_version() == 5
+
+
+def test_build_ids_match_the_tree():
+    """The libraries carry the hash of the sources, headers and flags of this tree (build.py
+    source_hash): a stale librtg.so / librth.so cannot pass for HEAD's."""
+    from raytracingrenderer_amd import build
+    assert N.rth().rth_build_id().decode() == build.source_hash("host")
+    assert N.rtg().rtg_build_id().decode() == build.source_hash("device")
+
+
+def test_tile_pixels_follow_the_render_order():
+    """rtg_tile_pixels (host-side, no GPU): tile by tile, row-major inside a tile, clipped at the
+    film edge; the stripes of N ranks partition the film's pixels."""
+    import numpy as np
+    from raytracingrenderer_amd.distributed import tile_pixels, tiles_for_rank
+    W, H = 100, 70  # 4 x 3 tiles, the last column / row clipped
+    t = np.array([5, 11], np.uint32)
+    got = tile_pixels(W, H, t)
+    want = [y * W + x for tt in (5, 11) for y in range((tt // 4) * 32, min((tt // 4) * 32 + 32, H))
+            for x in range((tt % 4) * 32, min((tt % 4) * 32 + 32, W))]
+    assert got.tolist() == want
+    for world in (1, 2, 3, 8):
+        allp = np.concatenate([tile_pixels(W, H, tiles_for_rank(W, H, r, world)) for r in range(world)])
+        assert np.array_equal(np.sort(allp), np.arange(W * H, dtype=np.uint32))
+    n = C.c_uint32(0)
+    bad = np.array([12], np.uint32)
+    assert N.rtg().rtg_tile_pixels(W, H, N.ptr(bad, C.c_uint32), 1, None, C.byref(n)) != 0
 
 
 def test_no_gpu_fails_loudly():

@@ -1,7 +1,8 @@
-"""N>1 path on CPU: two gloo ranks each render their interleaved 32x32 tiles (tile % 2 == rank)
-and reduce the float32 film to rank 0 with raytracingrenderer_amd.distributed — the same helpers
-bench.py uses over RCCL. The per-rank renderer here is the C oracle (no GPU in this container);
-the reduced film must equal a single full render bit for bit."""
+"""N>1 path on CPU: gloo ranks each render their diagonal 32x32 tile stripes and assemble the
+float32 film on rank 0 with raytracingrenderer_amd.distributed (FilmExchange: every rank's own
+tiles packed, gathered to rank 0 and scattered; the whole-film reduce of rounds 1-4 is kept) — the
+same helpers bench.py uses over RCCL. The per-rank renderer here is the C oracle (no GPU in this
+container); the assembled film must equal a single full render bit for bit."""
 import os
 import socket
 
@@ -36,6 +37,54 @@ def _worker(rank, world, port, out_path):
         np.save(out_path, t.numpy())
     dist.barrier()
     dist.destroy_process_group()
+
+
+class _OracleRanks:
+    """The surface FilmExchange reads from a RayTracer (width, height, film()), backed by the C
+    oracle's render of this rank's tiles."""
+
+    def __init__(self, film):
+        self._film = film
+        self.height, self.width = film.shape[:2]
+
+    def film(self):
+        return self._film, 3
+
+
+def _xworker(rank, world, port, out_path):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle.pyoracle import Oracle
+    from raytracingrenderer_amd import loadScene
+    from raytracingrenderer_amd.distributed import FilmExchange, tiles_for_rank
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=100, height=70)  # clipped edge tiles
+    tiles = tiles_for_rank(100, 70, rank, world)
+    film, _ = Oracle(s, 4, "rtm").render(3, seed=77, tiles=tiles)
+    # rank 0's target starts as garbage: the exchange must write every pixel
+    t = torch.full((70, 100, 3), float("nan"), dtype=torch.float32)
+    fx = FilmExchange(100, 70, rank, world)
+    fx.exchange(_OracleRanks(film), t, dist)
+    if rank == 0:
+        np.save(out_path, t.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_own_tile_exchange_is_bit_exact(tmp_path, world):
+    """Every rank sends only its own tiles' pixels (rtg_tile_pixels order, padded to the longest
+    list); rank 0 scatters them: the film equals one full render, bit for bit."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "film.npy")
+    mp.spawn(_xworker, args=(world, _free_port(), out), nprocs=world, join=True)
+    from oracle.pyoracle import Oracle
+    from raytracingrenderer_amd import loadScene
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=100, height=70)
+    full, _ = Oracle(s, 4, "rtm").render(3, seed=77)
+    got = np.load(out)
+    assert np.array_equal(got.view(np.uint32), full.view(np.uint32))
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -118,6 +167,40 @@ def test_librtg_handles_sum_to_one_render(world):
     assert np.array_equal(acc.view(np.uint32), full.view(np.uint32))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_device_gather_scatter_assemble_one_render(world):
+    """The device half of the own-tile exchange on one GPU: N handles render their stripes,
+    rtg_film_gather packs each rank's pixels on the device, the packed buffers are stacked (what
+    the RCCL gather does across GPUs) and rtg_film_scatter writes them into a film that starts as
+    NaN: the result equals one handle's full render, bit for bit."""
+    import ctypes as C
+    import torch
+    from raytracingrenderer_amd import RayTracer, loadScene
+    from raytracingrenderer_amd import _native as N
+    from raytracingrenderer_amd.distributed import FilmExchange, tiles_for_rank
+    W, H = 200, 136
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=W, height=H)
+    one = RayTracer(s, seed=9)
+    one.render(3, first_sample=0)
+    want = one.film()[0]
+    fx = [FilmExchange(W, H, r, world, device="cuda:0") for r in range(world)]
+    recv = torch.zeros((world, fx[0].maxpix * 3), dtype=torch.float32, device="cuda:0")
+    for r in range(world):
+        rt = RayTracer(s, seed=9)
+        rt.render(3, tiles=tiles_for_rank(W, H, r, world),
+                  first_sample=0, sync=False)  # queued: the gather must order after it
+        assert N.rtg().rtg_film_gather(rt.handle, C.c_void_p(fx[r].t_own.data_ptr()), fx[r].maxpix,
+                                       C.c_void_p(recv[r].data_ptr()), None) == 0
+        rt.synchronize()
+        del rt
+    film = torch.full((H, W, 3), float("nan"), dtype=torch.float32, device="cuda:0")
+    assert N.rtg().rtg_film_scatter(0, C.c_void_p(recv.data_ptr()), C.c_void_p(fx[0].t_all.data_ptr()),
+                                    len(fx[0].all), C.c_void_p(film.data_ptr()), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(film.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
 def test_native_tile_partition_matches_python():
     """rtg_tiles_for_rank (librtg, used by rtg_group and the CLI's -gpus) is the partition of
     distributed.tiles_for_rank (pure host code: no GPU needed)."""
@@ -131,9 +214,9 @@ def test_native_tile_partition_matches_python():
 @pytest.mark.gpu
 @pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
 def test_group_film_equals_one_device(devices):
-    """rtg_group: one device through an RCCL communicator (ncclCommInitAll + ncclReduce), or N
-    ranks rehearsed on the box's one GPU (host-memory sum): the reduced film equals one handle's
-    render of every tile, bit for bit."""
+    """rtg_group: one device through an RCCL communicator (ncclCommInitAll; one rank, so no
+    send/recv), or N ranks rehearsed on the box's one GPU (own tiles packed, moved by device copies,
+    scattered): the assembled film equals one handle's render of every tile, bit for bit."""
     from raytracingrenderer_amd import RayTracer, RayTracerGroup, loadScene
     s = loadScene(os.path.join(SCENES, "cornell-box"), width=200, height=136)
     one = RayTracer(s, seed=31)
@@ -184,8 +267,8 @@ def _visible_gpus():
 
 @pytest.mark.gpu
 def test_group_over_distinct_devices_equals_one_device():
-    """rtg_group over two distinct GPUs (ncclCommInitAll over devices 0 and 1, a real 2-rank
-    ncclReduce over xGMI): the reduced film equals one device's render, bit for bit. Needs >= 2
+    """rtg_group over two distinct GPUs (ncclCommInitAll over devices 0 and 1, rank 1's tiles sent
+    with ncclSend over xGMI): the assembled film equals one device's render, bit for bit. Needs >= 2
     visible GPUs (skipped on a one-GPU box; run on a node with several)."""
     if _visible_gpus() < 2:
         pytest.skip("needs >= 2 visible GPUs for a distinct-device RCCL group")

@@ -18,7 +18,7 @@ def kernels():
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
     from raytracingrenderer_amd.build import DEVICE_FLAGS  # each unit with the flags the build uses
-    res = {}
+    res = {"_asm": {}}
     for rel in ("device/rtg_kernels.hip", "device/rtg_shade.hip"):
         with tempfile.TemporaryDirectory() as d:
             out = os.path.join(d, "k.s")
@@ -27,6 +27,7 @@ def kernels():
                                                         os.path.join(DEVICE, os.path.basename(rel))],
                            check=True, capture_output=True)
             s = open(out).read()
+        res["_asm"][rel] = s
         md = s[s.index("amdhsa.kernels"):]
         for blk in md.split("  - .agpr_count")[1:]:
             name = re.search(r"\.name:\s+(\S+)", blk).group(1)
@@ -36,7 +37,7 @@ def kernels():
 
 
 def _find(kernels, prefix):
-    names = [k for k in kernels if k.startswith(prefix)]
+    names = [k for k in kernels if k.startswith(prefix) and k != "_asm"]
     assert names, prefix
     return kernels[names[0]]
 
@@ -52,3 +53,16 @@ def test_traversal_fits_six_waves_without_loop_spills(kernels):
 def test_shading_kernel_does_not_spill(kernels):
     k = _find(kernels, "_Z7k_shadeILb0E")
     assert k["vgpr_spill_count"] == 0 and k["private_segment_fixed_size"] == 0, k
+
+
+def test_shade_tables_are_waited_for_before_the_barrier(kernels):
+    """k_shade<.., TAB = true> fills its material / light tables with global_load_lds, which
+    completes on vmcnt; other waves read them after the block barrier. The instruction before that
+    first s_barrier must be an s_waitcnt with vmcnt(0) (rtg_shade.hip issues it explicitly)."""
+    s = kernels["_asm"]["device/rtg_shade.hip"]
+    for name in ("_Z7k_shadeILb0ELb1E", "_Z7k_shadeILb1ELb1E"):
+        body = s[s.index(name + "Ev"):]
+        body = body[body.index("global_load_lds_dwordx4"):]
+        pre = body[:body.index("s_barrier")].strip().splitlines()
+        waits = [l.strip() for l in pre if l.strip().startswith("s_waitcnt")]
+        assert waits and "vmcnt(0)" in waits[-1], (name, waits[-3:])

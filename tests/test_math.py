@@ -102,6 +102,24 @@ def test_special_cases():
             assert same_bits(np.array([a]), np.array([b])), (y, x, a, b)
 
 
+@pytest.mark.parametrize("stride", [31, 1])
+def test_division_rewrites_are_exact(stride):
+    """k_shade computes x / (float)M_PI, (double)x / M_PI and (double)x / (2 M_PI) as products with
+    the reciprocal (rtg_dev.h, "division by a constant"); oracle/div_rewrites checks that they return
+    the division's bits on every stride-th float input; stride 1 is all 2^32 inputs (~8 s on 8
+    threads; recorded in profiles/r05_div_rewrites_exhaustive.txt). Pure IEEE binary32/binary64
+    arithmetic, so the result holds on any host."""
+    exe = os.path.join(BUILD, "div_rewrites")
+    r = subprocess.run([exe, str(stride)], capture_output=True, text=True, timeout=900)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [l for l in r.stdout.splitlines() if "inputs" in l]
+    assert [l.split()[0] for l in lines] == ["pi_f", "pi_d", "twopi_d"]
+    for l in lines:
+        f = l.split()
+        assert int(f[2]) == ((1 << 32) + stride - 1) // stride and f[4] == "0", l
+
+
 def test_fused_sincos_is_bit_identical():
     """rtm_sincosf (one reduction, branch-free quadrant selects; what the device's
     spherical_to_world uses) returns the bits of rtm_sinf / rtm_cosf."""
