@@ -84,6 +84,8 @@ struct JVal {
 struct JParser {
     const std::string& s;
     size_t pos = 0;
+    int depth = 0;  // nesting of arrays / objects: deeper than kMaxDepth parses as null (no stack overflow)
+    static constexpr int kMaxDepth = 256;
     explicit JParser(const std::string& src) : s(src) {}
     char peek() const { return pos < s.size() ? s[pos] : 0; }
     char take() { return pos < s.size() ? s[pos++] : (pos++, 0); }
@@ -96,8 +98,9 @@ struct JParser {
         if (c == 't' || c == 'f') { v.kind = JVal::Bool; v.b = c == 't'; pos += c == 't' ? 4 : 5; return v; }
         if (c == '-' || std::isdigit((unsigned char)c)) return number();
         if (c == '"') return string();
-        if (c == '[') return array();
-        if (c == '{') return object();
+        if ((c == '[' || c == '{') && depth >= kMaxDepth) { pos = s.size(); return v; }
+        if (c == '[') { ++depth; JVal a = array(); --depth; return a; }
+        if (c == '{') { ++depth; JVal o = object(); --depth; return o; }
         return v;
     }
     JVal number() {
@@ -214,6 +217,12 @@ bool load_gem(const std::string& path, std::vector<GemMesh>& meshes, std::string
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) { err = path + " is not a GE Model File (missing)"; return false; }
     auto rd = [&](void* p, size_t n) { return std::fread(p, 1, n, f) == n; };
+    // the bytes left in the file bound every count read from it: a corrupted count fails as a
+    // truncated file instead of asking for gigabytes (found by tests/test_sanitize.py)
+    std::fseek(f, 0, SEEK_END);
+    const long fsize = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    auto left = [&]() -> size_t { const long at = std::ftell(f); return (at < 0 || fsize < at) ? 0 : (size_t)(fsize - at); };
     uint32_t magic = 0, animated = 0, n_meshes = 0;
     if (!rd(&magic, 4) || magic != kGemMagic) { std::fclose(f); err = path + " is not a GE Model File"; return false; }
     if (!rd(&animated, 4) || !rd(&n_meshes, 4)) { std::fclose(f); err = "truncated " + path; return false; }
@@ -224,14 +233,14 @@ bool load_gem(const std::string& path, std::vector<GemMesh>& meshes, std::string
         if (!rd(&n_props, 4)) break;
         for (uint32_t i = 0; i < 2 * n_props; ++i) {  // name, value strings
             int32_t len = 0;
-            if (!rd(&len, 4) || len < 0) { std::fclose(f); err = "bad string in " + path; return false; }
+            if (!rd(&len, 4) || len < 0 || (size_t)len > left()) { std::fclose(f); err = "bad string in " + path; return false; }
             std::fseek(f, len, SEEK_CUR);
         }
         uint32_t nv = 0, ni = 0;
-        if (!rd(&nv, 4)) { std::fclose(f); err = "truncated " + path; return false; }
+        if (!rd(&nv, 4) || (size_t)nv * sizeof(GemVertex) > left()) { std::fclose(f); err = "truncated " + path; return false; }
         mesh.vertices.resize(nv);
         if (nv && !rd(mesh.vertices.data(), (size_t)nv * sizeof(GemVertex))) { std::fclose(f); err = "truncated " + path; return false; }
-        if (!rd(&ni, 4)) { std::fclose(f); err = "truncated " + path; return false; }
+        if (!rd(&ni, 4) || (size_t)ni * 4 > left()) { std::fclose(f); err = "truncated " + path; return false; }
         mesh.indices.resize(ni);
         if (ni && !rd(mesh.indices.data(), (size_t)ni * 4)) { std::fclose(f); err = "truncated " + path; return false; }
         meshes.push_back(std::move(mesh));

@@ -9,6 +9,8 @@
 //   float -> RGBE uses frexp(max)*256/max, and scanline RLE only for 8 <= width < 32768.
 #include "image_io.h"
 
+#include <cstdint>
+
 #include <zlib.h>
 
 #include <cmath>
@@ -85,6 +87,10 @@ bool decode_png(const std::string& path, Image8& img, std::string& err) {
     if (!w || !h) { err = "PNG without IHDR"; return false; }
     if (interlace) { err = "interlaced PNG not supported: " + path; return false; }
     int samples = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
+    // stb_image's size limits (stb_image.h:5109-5126, STBI_MAX_DIMENSIONS = 1 << 24): a header the
+    // reference rejects is rejected here before anything is allocated
+    if (w > (1u << 24) || h > (1u << 24)) { err = "PNG too large (corrupt?): " + path; return false; }
+    if (samples && (1u << 30) / w / (ctype == 3 ? 4u : (unsigned)samples) < h) { err = "PNG too large to decode: " + path; return false; }
     if (!samples || !(depth == 8 || depth == 16 || (depth < 8 && (ctype == 0 || ctype == 3)))) {
         err = "unsupported PNG format in " + path;
         return false;
@@ -224,6 +230,11 @@ bool decode_hdr(const std::string& path, ImageF& img, std::string& err) {
     int h = 0, w = 0;
     if (std::sscanf(s.c_str(), "-Y %d +X %d", &h, &w) != 2 || w <= 0 || h <= 0) {
         err = "unsupported HDR orientation in " + path;
+        return false;
+    }
+    // stb_image's limits (stb_image.h:7197-7207): dimensions <= 1 << 24, w * h * 3 floats < 2^31 B
+    if (w > (1 << 24) || h > (1 << 24) || (uint64_t)w * (uint64_t)h * 12u > (uint64_t)INT32_MAX) {
+        err = "HDR image too large: " + path;
         return false;
     }
     img.width = w;

@@ -15,6 +15,7 @@
 // Written from the standard; only the numeric conventions above are taken from stb's behaviour.
 #include "image_io.h"
 
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -167,6 +168,9 @@ struct Decoder {
         if (img_x <= 0 || img_y <= 0) return fail("bad JPEG size");
         if (ncomp != 1 && ncomp != 3 && ncomp != 4) return fail("bad component count");
         if (len != 8 + 3 * ncomp) return fail("bad SOF length");
+        // stb_image's stbi__mad3sizes_valid(x, y, n): x * y * n within an int (stb_image.h:3298); the
+        // sample planes below are sized from the header, so a corrupt one fails before allocating
+        if ((int64_t)img_x * img_y * ncomp > (int64_t)INT32_MAX) return fail("JPEG too large to decode");
         hmax = vmax = 1;
         for (int i = 0; i < ncomp; ++i) {
             comp[i].id = u8();

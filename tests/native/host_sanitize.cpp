@@ -12,6 +12,7 @@
 #include "../../include/rth.h"
 
 #include <dirent.h>
+#include <time.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -113,8 +114,20 @@ std::vector<std::vector<unsigned char>> mutants(const std::vector<unsigned char>
 int g_fail = 0;
 long g_ok = 0, g_rejected = 0;
 
+double now_s() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
 void decode_file(const std::string& path, const std::string& ext) {
+    const double t0 = now_s();
+    struct Slow {
+        const std::string& p; double t0; int32_t* w; int32_t* h;
+        ~Slow() { if (getenv("HS_SLOW") && now_s() - t0 > 0.1) std::fprintf(stderr, "slow %.2fs %s %dx%d\n", now_s() - t0, p.c_str(), *w, *h); }
+    };
     int32_t w = 0, h = 0, c = 0;
+    Slow slow{path, t0, &w, &h};
     if (ext == "hdr") {
         float* px = nullptr;
         const int rc = rth_read_hdr(path.c_str(), &w, &h, &px);
@@ -145,7 +158,7 @@ void load_and_render(const std::string& dir, int width, int height, bool render,
     o.width = width;
     o.height = height;
     o.skip_missing = 1;
-    o.bvh_threads = 2;
+    o.bvh_threads = 1;
     o.envmap = envmap;
     rth_scene* s = nullptr;
     if (rth_load_scene(dir.c_str(), &o, &s) != 0) {
@@ -163,7 +176,7 @@ void load_and_render(const std::string& dir, int width, int height, bool render,
         if (os) {
             std::vector<float> film((size_t)info.width * info.height * 3, 0.0f);
             uint64_t counts[5] = {0, 0, 0, 0, 0};
-            if (or_render(os, 0, 1, 1234, nullptr, 0, 2, film.data(), counts, 1) != 0) g_fail = 1;
+            if (or_render(os, 0, 1, 1234, nullptr, 0, 1, film.data(), counts, 1) != 0) g_fail = 1;
             std::vector<uint8_t> rgb(film.size());
             rth_tonemap(info.width, info.height, film.data(), 1, 1.0f, rgb.data());
             or_destroy(os);
