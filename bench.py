@@ -39,13 +39,15 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")  # rocprofv
 KSTATS = os.path.join(ROOT, "profiles", "r04_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
 VALU_ISSUE = os.path.join(ROOT, "profiles", "r04_valu_issue.json")    # tools/valu_issue.py (SQ_INSTS_VALU passes)
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
-ROOF_REPLAY = os.path.join(ROOT, "profiles", "r04_roof_replay.jsonl")  # tools/roof_replay.py (C3)
-# the replay ceiling of each workload (tools/roof_replay.py on an MI355X), by (config, shard_of)
+ROOF_REPLAY = os.path.join(ROOT, "profiles", "r05_roof_replay_c3.jsonl")  # tools/roof_replay.py (C3)
+# the replay ceiling of each workload (tools/replay_all.sh on an MI355X: tools/roof_replay.py at the
+# line's own chunk shape), by (config, shard_of); a ceiling is quoted only when its chunk shape
+# (samples per chunk) is the line's
 ROOF_REPLAYS = {("C3", 1): ROOF_REPLAY,
-                ("C3", 8): os.path.join(ROOT, "profiles", "r04_roof_replay_shard8.jsonl"),
-                ("C2", 1): os.path.join(ROOT, "profiles", "r04_roof_replay_c2.jsonl"),
-                ("C4", 1): os.path.join(ROOT, "profiles", "r04_roof_replay_c4_32spp.jsonl"),
-                ("C5", 1): os.path.join(ROOT, "profiles", "r04_roof_replay_c5_4spp.jsonl")}
+                ("C3", 8): os.path.join(ROOT, "profiles", "r05_roof_replay_shard8.jsonl"),
+                ("C2", 1): os.path.join(ROOT, "profiles", "r05_roof_replay_c2.jsonl"),
+                ("C4", 1): os.path.join(ROOT, "profiles", "r05_roof_replay_c4_128spp.jsonl"),
+                ("C5", 1): os.path.join(ROOT, "profiles", "r05_roof_replay_c5_16spp.jsonl")}
 # k_shade's algorithmic bytes (PATH integrator; the payload travels with the queues):
 # every shaded path reads its pixel 4 and writes contrib 16 and meta 4 (k_accumulate reads the contrib
 # entry back: 16); every traced closest-hit ray's direction 16, hit record 16 and, on a hit, the
@@ -133,7 +135,7 @@ class GroupRender:
 
     def stats(self):
         self.last_ranks = self.g.rank_stats()
-        return {k: sum(r[k] for r in self.last_ranks) for k in self.last_ranks[0]}
+        return {k: (max if k == "chunk_samples" else sum)(r[k] for r in self.last_ranks) for k in self.last_ranks[0]}
 
     def film(self):
         return self.g.film()
@@ -287,7 +289,7 @@ def main():
     # timed region: per-launch HIP events on the render stream give the closest-hit kernel time
     rt.set_options(flags=base | N.RTG_OPT_TIMING)
     timing_xch[0] = True
-    ext_rays = shadow_rays = paths = cam_traced = 0
+    ext_rays = shadow_rays = paths = cam_traced = chunk_spp = 0
     extend_ms = shadow_ms = shade_ms = 0.0
     extend_launches = 0
     barrier_sync()
@@ -304,6 +306,7 @@ def main():
         shadow_ms += st["shadow_ms"]
         shade_ms += st["shade_ms"]
         extend_launches += st["extend_launches"]
+        chunk_spp = max(chunk_spp, st.get("chunk_samples", 0))
     barrier_sync()
     elapsed = time.perf_counter() - t_start
     timing_xch[0] = False
@@ -479,6 +482,8 @@ def main():
             replay = [json.loads(l) for l in open(replay_file) if '"total"' in l][-1]
         except Exception:
             replay = None
+    # a replay taken at another chunk shape walks other rays: it is not this line's ceiling
+    replay_shape_ok = bool(replay) and replay.get("chunk_spp") == chunk_spp and a.tris == 1_000_000
     # k_shade: algorithmic payload bytes per step (SHADE_B_*) / its kernel time (the timed region's
     # generate + shade + accumulate HIP events), and the PMC DRAM-level bytes of its launches
     shaded = ext_rays  # every closest-hit ray's result is shaded once
@@ -550,6 +555,7 @@ def main():
                            a.config, "synth-1M" if cfg["scene"] is None else cfg["scene"] + ("_f" if cfg.get("skip_missing") else ""),
                            a.width, a.height, a.spp, a.max_depth),
                        "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
+                       "chunk_spp": chunk_spp,
                        "max_depth": a.max_depth,
                        "parallelism": ("tile-sharded x%d + own-tile film exchange over %s" % (world, "RCCL" if backend == "nccl" else backend)
                                        if group_devs is None else
@@ -601,7 +607,9 @@ def main():
                              "replay_ceiling": (None if not replay else
                                                 {"peak": round(replay["ceiling_g_fetches_per_s"], 1),
                                                  "frac_vs_replay": (round(achieved_rec / replay["ceiling_g_fetches_per_s"], 4)
-                                                                    if achieved_rec else None),
+                                                                    if achieved_rec and replay_shape_ok else None),
+                                                 "chunk_spp": replay.get("chunk_spp"),
+                                                 "matches_line_chunk": replay_shape_ok,
                                                  "k_trace_ms": round(replay["k_trace_ms"], 2),
                                                  "replay_ms": round(replay["replay_ms"], 2),
                                                  "replayed_fetches": replay["replayed_fetches"],

@@ -35,7 +35,7 @@ extern "C" {
  * 4: rtg_render_async queues frames (returns before any of its work has run), rtg_render_idle,
  *    rtg_stats.traced_camera_rays appended;
  * 5: rtg_build_id; the own-tile film exchange (rtg_tile_pixels, rtg_film_gather, rtg_film_scatter),
- *    which rtg_group_reduce now uses in place of a whole-film ncclReduce */
+ *    which rtg_group_reduce now uses in place of a whole-film ncclReduce; rtg_stats.chunk_samples */
 #define RTG_ABI_VERSION 5
 
 /* error codes */
@@ -127,6 +127,8 @@ typedef struct rtg_stats {
                                    /* pixel centre's for every sample (Renderer.h:805-808), so a chunk  */
                                    /* traces one per pixel and its samples share the first hit;         */
                                    /* extension_rays counts one per sample, as the reference casts them */
+    uint64_t chunk_samples;        /* samples per pixel of the largest wavefront chunk issued since the */
+                                   /* last rtg_clear (ABI 5): the chunk shape of the render           */
 } rtg_stats;
 
 typedef struct rtg_handle rtg_handle;

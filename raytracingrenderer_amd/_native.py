@@ -56,7 +56,8 @@ class rtg_stats(C.Structure):
                 ("extend_ms", C.c_double), ("shadow_ms", C.c_double), ("shade_ms", C.c_double),
                 ("lane_slots", C.c_uint64), ("node_lane_steps", C.c_uint64), ("leaf_lane_steps", C.c_uint64),
                 ("leaf_phase_slots", C.c_uint64), ("pops", C.c_uint64), ("cullable_pops", C.c_uint64),
-                ("tri_tail_loads", C.c_uint64), ("leafbox_tests", C.c_uint64), ("traced_camera_rays", C.c_uint64)]
+                ("tri_tail_loads", C.c_uint64), ("leafbox_tests", C.c_uint64), ("traced_camera_rays", C.c_uint64),
+                ("chunk_samples", C.c_uint64)]
 
 
 class rth_load_options(C.Structure):

@@ -1686,6 +1686,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         ns_chunk = (n_samples + nchunks - 1) / nchunks;
     }
     const size_t P = (size_t)ns_chunk * h->npix;
+    h->stats.chunk_samples = std::max<uint64_t>(h->stats.chunk_samples, ns_chunk);
     // the frame pipeline (rtg_internal.h, ChunkSlot): queued chunks of up to RTG_PIPE_MAX_P paths
     // rotate through the slots with no host wait, so the next queued frames run beside them. A call
     // that is waited for runs its chunks one at a time in slot 0: chunks of one render side by side

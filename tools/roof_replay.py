@@ -66,7 +66,7 @@ def product(a):
     rt.render(a.spp, tiles=tl, first_sample=0)
     st = rt.stats()
     fetches = st["node_lane_steps"] + st["tri_tests"] + st["shadow_tri_tests"] + st["leafbox_tests"]
-    print(json.dumps({"launch_ms": best, "count_fetches": fetches,
+    print(json.dumps({"launch_ms": best, "count_fetches": fetches, "chunk_spp": st["chunk_samples"],
                       "rays": st["extension_rays"] + st["shadow_rays"]}), flush=True)
 
 
@@ -138,7 +138,13 @@ def main():
         print(json.dumps(r))
     ceiling = tot_replayed / tot_replay_ms / 1e6
     achieved = pr["count_fetches"] / tot_ms / 1e6
-    print(json.dumps({"total": True, "count_fetches": pr["count_fetches"], "replayed_fetches": tot_replayed,
+    n_launch = len(rows)
+    if len(pr["launch_ms"]) != n_launch:
+        sys.stderr.write("the render ran %d trace launches, the capture %d: more than one chunk, so the replay "
+                         "would not cover the timed launches; use --spp of one chunk\n" % (len(pr["launch_ms"]), n_launch))
+        sys.exit(3)
+    print(json.dumps({"total": True, "config": a.config, "spp": a.spp, "chunk_spp": pr.get("chunk_spp"),
+                      "shard_of": a.shard_of, "count_fetches": pr["count_fetches"], "replayed_fetches": tot_replayed,
                       "k_trace_ms": tot_ms, "replay_ms": tot_replay_ms,
                       "achieved_g_fetches_per_s": achieved, "ceiling_g_fetches_per_s": ceiling,
                       "frac": achieved / ceiling,
