@@ -136,6 +136,30 @@ def build_device(force=False, debug=False):
     return out
 
 
+def build_variant(name, extra_flags):
+    """A/B variant of librtg (tools/mkab.sh): the product's units and flags plus `extra_flags`
+    (e.g. -DRTG_FOO=1), into lib/ab/<name>.so; loaded through RTG_LIB by tools/ab*.sh."""
+    d = os.path.join(LIB, "ab")
+    os.makedirs(d, exist_ok=True)
+    out = os.path.join(d, name + ".so")
+    src = [os.path.join(CSRC, s) for s in DEVICE_SRC]
+    with tempfile.TemporaryDirectory() as tmp:
+        objs, procs = [], []
+        for rel, path in zip(DEVICE_SRC, src):
+            obj = os.path.join(tmp, os.path.basename(rel) + ".o")
+            cmd = ([HIPCC, "--offload-arch=" + ARCH] + DEVICE_CXXFLAGS + ['-DRTG_BUILD_ID="ab-%s"' % name] +
+                   list(extra_flags) + DEVICE_FLAGS.get(rel, []) + ["-c", "-o", obj, path])
+            procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+            objs.append(obj)
+        for cmd, pr in procs:
+            log = pr.communicate()[0]
+            if pr.returncode != 0:
+                sys.stderr.write(log)
+                raise RuntimeError("build failed: " + " ".join(cmd))
+        _run([HIPCC, "--offload-arch=" + ARCH, "-fPIC", "-shared", "-o", out] + objs + DEVICE_LDFLAGS)
+    return out
+
+
 def build_cli(force=False):
     out = os.path.join(LIB, "rtg_render")
     src = [os.path.join(CSRC, "host", "cli.cpp")]

@@ -950,13 +950,43 @@ static void host_cross(const float* a, const float* b, float* o) {
 // is exact) and k_trace's leaf-box test keeps reachability the reference's. The reference splits
 // along the longest axis only (Geometry.h:343-386); this build tries all three: full SAH sweep
 // below 2048 leaves, 64 centroid bins per axis above.
+#ifndef RTG_TRI_LEAVES
+#define RTG_TRI_LEAVES 0
+#endif
 static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& lk, std::vector<float>& bd) {
-    std::vector<int> leaf;
-    for (uint32_t i = 0; i < d->n_nodes; ++i)
-        if (d->node_links[(size_t)i * 4] < 0) leaf.push_back((int)i);
-    const size_t n = leaf.size();
+    // primitives: the reference leaves (box, links {-1, -1, start, end}); RTG_TRI_LEAVES: every
+    // triangle alone, its box inflated by 2^-17 of the scene scale (a hit that rayIntersect reports
+    // lies within rounding of its triangle)
+    std::vector<float> pbox;
+    std::vector<std::array<int32_t, 4>> plink;
+    if (RTG_TRI_LEAVES) {
+        float scale = 0.0f;
+        for (int k = 0; k < 6; ++k)
+            if (std::isfinite(d->node_bounds[k])) scale = std::max(scale, std::fabs(d->node_bounds[k]));
+        const double eps = std::ldexp((double)scale, -17);
+        for (uint32_t t = 0; t < d->n_tris; ++t) {
+            const float* P = d->positions + (size_t)t * 9;
+            for (int a = 0; a < 3; ++a) {
+                const double lo = std::min(std::min(P[a], P[3 + a]), P[6 + a]) - eps;
+                pbox.push_back(std::nextafter((float)lo, -INFINITY));
+            }
+            for (int a = 0; a < 3; ++a) {
+                const double hi = std::max(std::max(P[a], P[3 + a]), P[6 + a]) + eps;
+                pbox.push_back(std::nextafter((float)hi, INFINITY));
+            }
+            plink.push_back({-1, -1, (int32_t)t, (int32_t)t + 1});
+        }
+    } else {
+        for (uint32_t i = 0; i < d->n_nodes; ++i) {
+            const int32_t* L = d->node_links + (size_t)i * 4;
+            if (L[0] >= 0) continue;
+            pbox.insert(pbox.end(), d->node_bounds + (size_t)i * 6, d->node_bounds + (size_t)i * 6 + 6);
+            plink.push_back({L[0], L[1], L[2], L[3]});
+        }
+    }
+    const size_t n = plink.size();
     if (n < 2) return false;
-    auto box = [&](int p) { return d->node_bounds + (size_t)leaf[p] * 6; };
+    auto box = [&](int p) { return pbox.data() + (size_t)p * 6; };
     std::vector<float> cen(n * 3);
     for (size_t p = 0; p < n; ++p)
         for (int a = 0; a < 3; ++a) cen[p * 3 + a] = 0.5f * (box((int)p)[a] + box((int)p)[a + 3]);
@@ -975,10 +1005,7 @@ static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& l
     // bins per axis above (a full sweep to 16384 leaves or 256 bins measured no better)
     const int sweep_max = 2048, nbins = 64;
     std::vector<double> wt(n), pre;
-    for (size_t p = 0; p < n; ++p) {
-        const int32_t* L = d->node_links + (size_t)leaf[p] * 4;
-        wt[p] = (double)(L[3] - L[2]);
-    }
+    for (size_t p = 0; p < n; ++p) wt[p] = (double)(plink[p][3] - plink[p][2]);
     std::vector<int> idx(n);
     for (size_t p = 0; p < n; ++p) idx[p] = (int)p;
     lk.assign((2 * n - 1) * 4, -1);
@@ -995,8 +1022,7 @@ static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& l
         for (int p = lo; p < hi; ++p) all.add(box(idx[p]));
         std::memcpy(&bd[(size_t)node * 6], all.b, sizeof(all.b));
         if (m == 1) {
-            const int32_t* L = d->node_links + (size_t)leaf[idx[lo]] * 4;
-            std::memcpy(&lk[(size_t)node * 4], L, 4 * sizeof(int32_t));
+            std::memcpy(&lk[(size_t)node * 4], plink[idx[lo]].data(), 4 * sizeof(int32_t));
             continue;
         }
         double best = INFINITY;

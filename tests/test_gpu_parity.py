@@ -141,6 +141,39 @@ def test_wide_walk_adversarial_rays(synth20k, cornell256):
             assert np.array_equal(a.trace_visible(r), b.trace_visible(r))
 
 
+def test_wide_walk_triangle_grazing_rays(synth20k, cornell256):
+    """Rays aimed exactly at triangle vertices and edge points (and a hair inside / outside them),
+    from near and far origins, along generic and nearly axis-parallel directions: rayIntersect's
+    accept / reject decisions at the triangle boundary must be reached by the compressed walk
+    whatever boxes its slots hold (reference leaves, or single triangles with inflated boxes)."""
+    rng = np.random.default_rng(33)
+    for s in (synth20k, cornell256):
+        P = s.positions.reshape(-1, 3, 3).astype(np.float64)
+        n = 60000
+        t = rng.integers(0, len(P), n)
+        i, j = rng.integers(0, 3, n), rng.integers(0, 3, n)
+        w = rng.choice([0.0, 0.5, 1.0], n) * (rng.random(n) < 0.5) + rng.random(n) * (rng.random(n) >= 0.5)
+        tgt = P[t, i] + w[:, None] * (P[t, j] - P[t, i])  # a vertex or a point of an edge
+        cen = P[t].mean(axis=1)
+        tgt = tgt + (tgt - cen) * rng.choice([0.0, 1e-7, -1e-7, 1e-6], n)[:, None]  # on / just off the edge
+        ext = float(np.abs(s.node_bounds[0]).max())
+        dist = ext * 10.0 ** rng.uniform(-3, 1, n)
+        d = rng.normal(size=(n, 3))
+        ax = rng.random(n) < 0.3
+        d[ax] = np.eye(3)[rng.integers(0, 3, ax.sum())] + 1e-4 * rng.normal(size=(ax.sum(), 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        o = tgt - d * dist[:, None]
+        r = np.zeros((n, 8), np.float32)
+        r[:, :3] = o
+        r[:, 4:7] = d
+        r[:, 3] = (dist * 1.5).astype(np.float32)
+        for cull in (True, False):
+            a = RayTracer(s, cull=cull, wide=True)
+            b = RayTracer(s, cull=cull, wide=False)
+            assert_bitexact(a.trace_closest(r), b.trace_closest(r), "grazing closest")
+            assert np.array_equal(a.trace_visible(r), b.trace_visible(r))
+
+
 @pytest.mark.parametrize("max_depth", [0, 1, 8, 16])
 def test_depths_cornell_materials(max_depth):
     """glass / mirror / Lambert stubs (one- and two-sided) / env + area lights (configs C2, C4 depth)."""

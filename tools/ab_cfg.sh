@@ -16,5 +16,5 @@ for lib in raytracingrenderer_amd/lib/ab/*.so; do
   RTG_LIB=$R/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --dropin-frames 0 $args > gpurun_out/ab.log 2> gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 1; }
   echo "$cfg $(basename $lib) $(tail -1 gpurun_out/ab.log | python3 -c "
 import json,sys
-d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['kernel_ms_per_step_rank0'])")"
+d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], d['ms_per_step'], d['kernel_ms_per_step_rank0'], 'fetch/ray', r['fetches']['per_ray'], 'node', r['node_steps_per_ray'], 'tri', r['walk_tri_tests_per_ray'], 'util', r['lane_util_node_leaf'])")"
 done; done; done

@@ -1,13 +1,12 @@
 #!/bin/bash
-# build A/B variants of librtg into raytracingrenderer_amd/lib/ab: mkab.sh name "-DFOO=1" [name "-D..."]...
+# build A/B variants of librtg into raytracingrenderer_amd/lib/ab (the product's units and per-unit
+# flags, build.py build_variant): mkab.sh name "-DFOO=1" [name "-D..."]...  ("" = the product as is)
 set -e
 cd "$(dirname "$0")/.."
-mkdir -p raytracingrenderer_amd/lib/ab
-D=raytracingrenderer_amd/csrc/device
+rm -rf raytracingrenderer_amd/lib/ab; mkdir -p raytracingrenderer_amd/lib/ab
 while [ $# -ge 2 ]; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -fPIC -shared $2 \
-    -o raytracingrenderer_amd/lib/ab/$1.so $D/rtg_kernels.hip $D/rtg_shade.hip $D/rtg_light.hip $D/rtg_multi.hip \
-    -ldl -Wl,-rpath,/opt/rocm/lib &
+  python3 -c "import sys; from raytracingrenderer_amd import build; build.build_variant(sys.argv[1], sys.argv[2].split())" "$1" "$2" &
   shift 2
 done
 wait
+ls raytracingrenderer_amd/lib/ab
