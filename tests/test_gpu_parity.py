@@ -96,8 +96,9 @@ def test_wide_walk_is_exact(cornell256, synth20k):
 
 
 def test_wide_walk_over_own_tree_equals_bvh2_walk(synth20k, cornell256):
-    """Wide nodes cut from the own 3-axis SAH tree over the reference leaves return the reference
-    BVH2 walk's bits: films and 100k random closest-hit / any-hit queries per scene."""
+    """Wide nodes cut from the own 3-axis SAH tree over the triangles (one triangle per leaf slot,
+    inflated boxes; round 5) return the reference BVH2 walk's bits: films and 100k random closest-hit
+    / any-hit queries per scene."""
     rng = np.random.default_rng(31)
     for s in (synth20k, cornell256):
         assert_bitexact(gpu_film(s, 2, wide=True), gpu_film(s, 2, wide=False), "bvh4 vs bvh2 film")
