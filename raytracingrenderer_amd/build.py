@@ -28,7 +28,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("RTG_ARCH", "gfx950")
 
 HOST_SRC = ["host/image_io.cpp", "host/jpeg_decode.cpp", "host/gem_json.cpp", "host/scene_front.cpp"]
-DEVICE_SRC = ["device/rtg_kernels.hip", "device/rtg_shade.hip", "device/rtg_light.hip", "device/rtg_multi.hip"]
+DEVICE_SRC = ["device/rtg_kernels.hip", "device/rtg_shade.hip", "device/rtg_light.hip", "device/rtg_multi.hip",
+              "device/rtg_bvh.hip"]
 # per-unit compile flags: k_shade's translation unit takes LLVM's max-ilp scheduler, which its
 # latency-bound body prefers, while the traversal keeps the default
 DEVICE_FLAGS = {"device/rtg_shade.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}

@@ -62,6 +62,25 @@ using namespace rtgd;
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 7   // min waves per SIMD for k_shade (72 VGPRs, no spills; one tile per block)
 #endif
+// The own binary tree the wide nodes are cut from (prepare_scene; rtg_bvh.hip for spatial splits)
+#ifndef RTG_SAH_SWEEP
+#define RTG_SAH_SWEEP 2048  // full SAH sweep up to this many primitives in a node, binned above
+#endif
+#ifndef RTG_SAH_BINS
+#define RTG_SAH_BINS 64     // centroid bins per axis of the binned SAH
+#endif
+#ifndef RTG_SBVH
+#define RTG_SBVH 0          // 1: spatial splits (rtg_bvh.hip build_sbvh)
+#endif
+#ifndef RTG_SBVH_BINS
+#define RTG_SBVH_BINS 32    // slabs per axis of a spatial split
+#endif
+#ifndef RTG_SBVH_ALPHA
+#define RTG_SBVH_ALPHA 1e-5 // spatial splits are tried when the object split's two boxes overlap by
+#endif                      // more than this fraction of the root box's area
+#ifndef RTG_SBVH_DUP
+#define RTG_SBVH_DUP 0.5    // at most this many extra references per triangle in all
+#endif
 // RTG_DEBUG=1 (a diagnostic build only) compiles k_trace's per-wave clocks (RTG_OPT_WAVETIME) and
 // the fetch capture + replay of the locality-matched roofline (RTG_OPT_CAPTURE, rtg_debug_replay).
 #define RTG_CAP_LEN 64
@@ -361,6 +380,8 @@ struct HostScene {
     rtg_camera_proj proj{};
 };
 
+// rtg_bvh.hip: the own binary tree with spatial splits over the triangles (descriptor node format)
+bool build_sbvh(const rtg_scene_desc* d, std::vector<int32_t>& lk, std::vector<float>& bd);
 // rtg_kernels.hip
 int prepare_scene(const rtg_scene_desc* d, HostScene& hs);
 int upload_scene(int device, const HostScene& hs, rtg_handle* h);

@@ -1010,7 +1010,7 @@ static bool rebuild_over_leaves(const rtg_scene_desc* d, std::vector<int32_t>& l
     };
     // SAH weight of a leaf: its triangle count (1-2); full sweep below 2048 leaves, 64 centroid
     // bins per axis above (a full sweep to 16384 leaves or 256 bins measured no better)
-    const int sweep_max = 2048, nbins = 64;
+    const int sweep_max = RTG_SAH_SWEEP, nbins = RTG_SAH_BINS;
     std::vector<double> wt(n), pre;
     for (size_t p = 0; p < n; ++p) wt[p] = (double)(plink[p][3] - plink[p][2]);
     std::vector<int> idx(n);
@@ -1233,7 +1233,7 @@ int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
         // (rebuild_over_leaves), or the reference BVH2 when that tree cannot be built
         std::vector<int32_t> rlk;
         std::vector<float> rbd;
-        const bool rebuilt = rebuild_over_leaves(d, rlk, rbd);
+        const bool rebuilt = (RTG_SBVH && build_sbvh(d, rlk, rbd)) || rebuild_over_leaves(d, rlk, rbd);
         const int32_t* LK = rebuilt ? rlk.data() : d->node_links;
         const float* BD = rebuilt ? rbd.data() : d->node_bounds;
         const uint32_t nn = rebuilt ? (uint32_t)(rlk.size() / 4) : d->n_nodes;
