@@ -199,11 +199,10 @@ struct Builder {
     // spans; entering / leaving counts give the two sides' reference counts at each plane
     double spatial_split(const std::vector<Ref>& r, const Box& nb, int& ax, double& plane) const {
         const int NB = RTG_SBVH_BINS;
-        double best = INFINITY;
-        ax = -1;
-        for (int a = 0; a < 3; ++a) {
+        auto axis = [&](int a, double& pl) -> double {
+            double best = INFINITY;
             const double lo = nb.lo[a], ext = nb.hi[a] - nb.lo[a];
-            if (!(ext > 0.0)) continue;
+            if (!(ext > 0.0)) return best;
             const double w = ext / NB;
             std::vector<Box> bins(NB);
             std::vector<long> enter(NB, 0), leave(NB, 0);
@@ -237,9 +236,23 @@ struct Builder {
                 lc += enter[b - 1];
                 if (lc == 0 || rc[b] == 0 || lc >= (long)r.size() || rc[b] >= (long)r.size()) continue;
                 const double c = left.area() * (double)lc + right[b].area() * (double)rc[b];
-                if (c < best) { best = c; ax = a; plane = lo + w * b; }
+                if (c < best) { best = c; pl = lo + w * b; }
             }
+            return best;
+        };
+        double cost[3], pl[3] = {0, 0, 0};
+        if (r.size() > 65536) {  // the top of the tree: the three axes on threads
+            std::thread t1([&] { cost[1] = axis(1, pl[1]); }), t2([&] { cost[2] = axis(2, pl[2]); });
+            cost[0] = axis(0, pl[0]);
+            t1.join();
+            t2.join();
+        } else {
+            for (int a = 0; a < 3; ++a) cost[a] = axis(a, pl[a]);
         }
+        double best = INFINITY;
+        ax = -1;
+        for (int a = 0; a < 3; ++a)  // the first axis of the lowest cost, as a serial loop would pick
+            if (cost[a] < best) { best = cost[a]; ax = a; plane = pl[a]; }
         return best;
     }
 

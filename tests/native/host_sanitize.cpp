@@ -216,14 +216,18 @@ int main(int argc, char** argv) {
     }
     int k = 0;
     for (int a = 2; a < argc; ++a) {
-        const std::string dir = argv[a];
+        // absolute: the mutant scenes are directories of symlinks to this one's files
+        char real[4096];
+        const std::string dir = realpath(argv[a], real) ? std::string(real) : std::string(argv[a]);
         std::fprintf(stderr, "[host_sanitize] %s\n", dir.c_str());
         load_and_render(dir, 48, 36, true);
         std::vector<std::pair<size_t, std::string>> gems;
+        size_t scene_bytes = 0;
         for (const std::string& f : list_dir(dir)) {
             const std::string p = dir + "/" + f, e = lower_ext(f);
             struct stat st{};
             if (stat(p.c_str(), &st) != 0 || !S_ISREG(st.st_mode)) continue;
+            scene_bytes += (size_t)st.st_size;
             if (e == "png" || e == "jpg" || e == "jpeg" || e == "hdr") {
                 decode_file(p, e);
                 // every texture of the scene, mutated (large files: fewer mutants)
@@ -238,14 +242,16 @@ int main(int argc, char** argv) {
             }
             ++k;
         }
-        // scene.json and the two smallest meshes, mutated, loaded as the scene
+        // scene.json and the two smallest meshes, mutated, loaded as the scene (every load decodes the
+        // scene's textures: fewer mutants for the big reference scenes)
+        const bool big = scene_bytes > (8u << 20);
         std::sort(gems.begin(), gems.end());
         std::vector<std::string> victims = {"scene.json"};
         for (size_t i = 0; i < gems.size() && i < 2; ++i) victims.push_back(gems[i].second);
         for (const std::string& v : victims) {
             const auto src = slurp(dir + "/" + v);
             if (src.empty()) continue;
-            for (const auto& m : mutants(src, 5000 + k, v == "scene.json" ? 60 : 24)) {
+            for (const auto& m : mutants(src, 5000 + k, v == "scene.json" ? (big ? 10 : 60) : (big ? 4 : 24))) {
                 load_and_render(shadow_scene(scratch, dir, v, m, k % 4), 24, 16, false);
                 ++k;
             }

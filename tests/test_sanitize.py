@@ -42,9 +42,12 @@ def test_committed_scenes_and_mutants_are_clean(driver, tmp_path):
 
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(ASSETS, "bathroom")), reason="reference scenes not staged")
+@pytest.mark.skipif(os.environ.get("RTG_SANITIZE_ASSETS") != "1",
+                    reason="~6 min under ASan: run with RTG_SANITIZE_ASSETS=1 (recorded in profiles/r05_host_sanitize.txt)")
 def test_reference_scenes_jpeg_png_hdr_mutants_are_clean(driver, tmp_path):
     """bathroom_f (baseline and progressive JPEGs, PNG masks), coffee_f + GI.hdr, materialball_f
-    (envmap.hdr) and their corrupted copies."""
+    (envmap.hdr) and their corrupted copies; every scene.json / .gem mutant is a full scene load
+    (textures decoded)."""
     scenes = [os.path.join(ASSETS, s) for s in ("bathroom", "coffee", "materialball")
               if os.path.isdir(os.path.join(ASSETS, s))]
     ok, rejected = _run(driver, tmp_path, scenes, 2400)
