@@ -220,6 +220,20 @@ def build_sanitized(force=False):
     return out
 
 
+def build_sbvh_check(force=False):
+    """Test infrastructure: tests/native/sbvh_check (rtg_bvh.hip's host code + librth, no GPU code
+    run) into tests/native/_build/; tests/test_bvh.py runs it."""
+    nat = os.path.join(ROOT, "tests", "native")
+    out_dir = os.path.join(nat, "_build")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, "sbvh_check")
+    src = [os.path.join(nat, "sbvh_check.cpp"), os.path.join(CSRC, "device", "rtg_bvh.hip")]
+    if force or _newer(out, _deps(src) + [os.path.join(LIB, "librth.so")]):
+        _run([HIPCC, "-O2", "-std=c++17", "-ffp-contract=off", "-o", out] + src +
+             ["-L" + LIB, "-lrth", "-Wl,-rpath," + LIB])
+    return out
+
+
 def build_ref(force=False):
     """oracle/_ref: the reference's own compilable headers, only when /root/reference exists."""
     mk = os.path.join(ORACLE, "ref", "Makefile")

@@ -70,7 +70,7 @@ using namespace rtgd;
 #define RTG_SAH_BINS 64     // centroid bins per axis of the binned SAH
 #endif
 #ifndef RTG_SBVH
-#define RTG_SBVH 0          // 1: spatial splits (rtg_bvh.hip build_sbvh)
+#define RTG_SBVH 1          // spatial splits (rtg_bvh.hip build_sbvh); 0: object splits only
 #endif
 #ifndef RTG_SBVH_BINS
 #define RTG_SBVH_BINS 32    // slabs per axis of a spatial split

@@ -1,7 +1,8 @@
-// sbvh_check — CPU check of rtg_bvh.hip's build_sbvh on a loaded scene (no GPU): the tree is well
-// formed (every internal box holds its children's, every triangle reachable), and every triangle is
-// covered by its leaf slots (random points of the triangle lie in one of its fragments' boxes), plus
-// build time and duplication. Build: tools/sbvh/build.sh; run: sbvh_check <scene dir> [w h] [synth n]
+// sbvh_check — TEST INFRASTRUCTURE ONLY (tests/test_bvh.py). CPU check of rtg_bvh.hip's build_sbvh on
+// a loaded scene (no GPU): the tree is well formed (every internal box holds its children's, every
+// triangle reachable), and every triangle is covered by its leaf slots (its vertices and random points
+// of it lie in one of its fragments' boxes), plus build time and duplication. Built by build.py
+// build_sbvh_check; run: sbvh_check <scene dir> | sbvh_check x synth <n triangles>
 #include "../../include/rth.h"
 #include "../../raytracingrenderer_amd/csrc/device/rtg_internal.h"
 
