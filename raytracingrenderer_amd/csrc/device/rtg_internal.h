@@ -67,10 +67,13 @@ using namespace rtgd;
 #define RTG_SAH_SWEEP 2048  // full SAH sweep up to this many primitives in a node, binned above
 #endif
 #ifndef RTG_SAH_BINS
-#define RTG_SAH_BINS 64     // centroid bins per axis of the binned SAH
+#define RTG_SAH_BINS 128    // centroid bins per axis of the binned SAH (64: C5 -2.3 %)
 #endif
 #ifndef RTG_SBVH
 #define RTG_SBVH 1          // spatial splits (rtg_bvh.hip build_sbvh); 0: object splits only
+#endif
+#ifndef RTG_LEAF_ORDER
+#define RTG_LEAF_ORDER 0    // 1: leaf-ordered triangle / leaf-box copies for the wide walk (big scenes)
 #endif
 #ifndef RTG_SBVH_BINS
 #define RTG_SBVH_BINS 32    // slabs per axis of a spatial split
