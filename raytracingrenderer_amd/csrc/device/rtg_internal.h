@@ -72,9 +72,6 @@ using namespace rtgd;
 #ifndef RTG_SBVH
 #define RTG_SBVH 1          // spatial splits (rtg_bvh.hip build_sbvh); 0: object splits only
 #endif
-#ifndef RTG_LEAF_ORDER
-#define RTG_LEAF_ORDER 0    // 1: leaf-ordered triangle / leaf-box copies for the wide walk (big scenes)
-#endif
 #ifndef RTG_SBVH_BINS
 #define RTG_SBVH_BINS 32    // slabs per axis of a spatial split
 #endif

@@ -231,26 +231,22 @@ void k_trace(SceneView s, TraceIO io) {
                     return anyr ? (tt < tbest && tt > RTG_EPS) : (tt <= tbest && tt > RTG_EPS);
                 }, t, u, v, c_tails);
                 if (hit) {
-                    // wide walk: tri indexes the leaf-ordered copies, and the reference id comes with
-                    // the leaf box; a tie (t == tbest) is decided by it after the gate
                     bool cand = anyr ? !(t >= tbest || t <= RTG_EPS)
-                                     : (t > RTG_EPS && (t < tbest || (t == tbest && (wide || tri < bid))));
-                    int ref = tri;
+                                     : (t > RTG_EPS && (t < tbest || (t == tbest && tri < bid)));
                     if (cand && wide) {
                         // the exact box of the reference leaf holding this triangle (stored per
-                        // triangle record, with the triangle's reference id)
+                        // triangle: a wide leaf slot may join sibling reference leaves)
                         const float4 b0 = lboxes[2 * tri], b1 = lboxes[2 * tri + 1];
                         if (COUNT) c_lbox += 1;
                         capture(2u, (unsigned)tri);
-                        ref = __float_as_int(b1.z);
-                        cand = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv) && (anyr || t < tbest || ref < bid);
+                        cand = slab_exact(b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, o, inv);
                     }
                     if (!cand) {
                     } else if (anyr) {
                         occluded = true;
                     } else {
                         tbest = t;
-                        bid = ref;
+                        bid = tri;
                         bu = u;
                         bv = v;
                         delta = RTG_CULL_REL * (omag + tbest * dmag);
@@ -1305,35 +1301,10 @@ int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
         const float* b = d->node_bounds + (size_t)i * 6;
         for (int t = L[2]; t < L[3]; ++t) {
             leafbox[2 * (size_t)t] = make_float4(b[0], b[1], b[2], b[3]);
-            leafbox[2 * (size_t)t + 1] = make_float4(b[4], b[5], host_bits_f(t), 0.0f);  // .z: the reference id
+            leafbox[2 * (size_t)t + 1] = make_float4(b[4], b[5], 0.0f, 0.0f);
         }
     }
-    // Leaf-ordered copies (RTG_LEAF_ORDER, big scenes): the triangle and leaf-box records of the wide
-    // leaf slots are copied after the reference-ordered ones in the order of the wide nodes (the slots
-    // of a node, then the next node's), and the slots' leaf words point at the copies, so the
-    // triangles a wide node reaches sit together in memory. The reference-ordered records stay for
-    // the exact BVH2 walk. The copy's leaf box carries its triangle's reference id (.z of its second
-    // half), which the walk's candidate test reads for hits and ties (k_trace leaf()).
     const bool small = hs.usew && nodesq.size() * 4 + (size_t)nt * 5 <= RTG_SMALL_F4;
-    if (RTG_LEAF_ORDER && hs.usew && !small) {
-        for (DevNodeQ& q : nodesq) {
-            float* w[4] = {&q.q[2].z, &q.q[2].w, &q.q[3].x, &q.q[3].y};
-            for (int k = 0; k < 4; ++k) {
-                int32_t word;
-                std::memcpy(&word, w[k], 4);
-                if (word >= 0 || word == RTG_EXIT) continue;
-                const int code = ~word, start = code / RTG_LEAF_SPAN, cnt = code % RTG_LEAF_SPAN + 1;
-                const size_t at = tris48.size();
-                for (int j = 0; j < cnt; ++j) {
-                    tris48.push_back(tris48[(size_t)start + j]);
-                    leafbox.push_back(leafbox[2 * ((size_t)start + j)]);
-                    leafbox.push_back(leafbox[2 * ((size_t)start + j) + 1]);
-                }
-                if (at * RTG_LEAF_SPAN > (size_t)INT32_MAX - RTG_LEAF_SPAN) { g_err = "scene too large"; return RTG_ERR_ARG; }
-                *w[k] = host_bits_f(~(int32_t)(at * RTG_LEAF_SPAN + (cnt - 1)));
-            }
-        }
-    }
     float scale = 0.0f;
     for (int k = 0; k < 6; ++k) {
         float v = std::fabs(d->node_bounds[k]);

@@ -15,9 +15,10 @@
 // queued frames a call returns once the frame three before it has left the GPU, so in the steady
 // state it is the GPU's time per frame.
 // Multi-GPU (one node): -gpus N renders on devices 0..N-1, -devices a,b,... on a list. Rank r
-// renders the 32x32 tiles with (tile_x + tile_y) % N == r, one host thread per device, and the films
-// are summed into the first device by one RCCL reduce before the film is written (rtg_group_*,
-// include/rtg.h); the output is bit-identical to the one-device render.
+// renders the 32x32 tiles with (tile_x + tile_y) % N == r, one host thread per device, and the film is
+// assembled on the first device from every device's own tiles (packed, one RCCL send per device,
+// scattered) before it is written (rtg_group_*, include/rtg.h); the output is bit-identical to the
+// one-device render.
 #include "../../../include/rth.h"
 
 #include <chrono>
@@ -85,8 +86,8 @@ int main(int argc, char** argv) {
         if (rtg_group_create(devices.data(), (int)devices.size(), rth_scene_desc(scene), &grp) != 0)
             return die("rtg_group_create", rtg_last_error());
         if (rtg_group_set_options(grp, max_depth, RTG_OPT_CULL, 0) != 0) return die("rtg_group_set_options", rtg_last_error());
-        std::printf("%d devices, film reduce by %s\n", (int)devices.size(),
-                    rtg_group_uses_rccl(grp) ? "RCCL (ncclReduce)" : "host memory (repeated devices)");
+        std::printf("%d devices, own-tile film exchange by %s\n", (int)devices.size(),
+                    rtg_group_uses_rccl(grp) ? "RCCL (ncclSend/ncclRecv)" : "device copies (repeated devices)");
     }
     std::printf("scene %s: %u triangles, %u lights, %dx%d (load %.0f ms, BVH %.0f ms)\n", scene_name.c_str(),
                 info.n_tris, info.n_lights, info.width, info.height, info.load_ms, info.bvh_ms);
@@ -116,7 +117,7 @@ int main(int argc, char** argv) {
                 (double)spp * info.width * info.height / wall / 1e6);
     if (grp) {
         if (rtg_group_film_read(grp, film.data(), &got) != 0) return die("rtg_group_film_read", rtg_last_error());
-        std::printf("film reduce: %.3f ms\n", rtg_group_reduce_ms(grp));
+        std::printf("film exchange: %.3f ms\n", rtg_group_reduce_ms(grp));
     } else if (rtg_film_read(rt, film.data(), &got) != 0) {
         return die("rtg_film_read", rtg_last_error());
     }
