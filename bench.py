@@ -35,9 +35,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, same guide (§L2)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")  # rocprofv3 PMC passes of the C3 bench
-KSTATS = os.path.join(ROOT, "profiles", "r04_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
-VALU_ISSUE = os.path.join(ROOT, "profiles", "r04_valu_issue.json")    # tools/valu_issue.py (SQ_INSTS_VALU passes)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")  # rocprofv3 PMC passes of the C3 bench
+KSTATS = os.path.join(ROOT, "profiles", "r05_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
+VALU_ISSUE = os.path.join(ROOT, "profiles", "r05_valu_issue.json")    # tools/valu_issue.py (SQ_INSTS_VALU passes)
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
 ROOF_REPLAY = os.path.join(ROOT, "profiles", "r05_roof_replay_c3.jsonl")  # tools/roof_replay.py (C3)
 # the replay ceiling of each workload (tools/replay_all.sh on an MI355X: tools/roof_replay.py at the
