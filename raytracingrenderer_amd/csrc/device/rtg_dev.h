@@ -114,9 +114,10 @@ struct __align__(16) DevMat {
     int kind, two_sided, tex, is_light;
     float int_ior, ext_ior;
     int tex_wh;  // the albedo texture's width | height << 16; `tex` is its first texel in SceneView::texels
-    int pad;
+    int uniform;  // 1: every texel of the texture has the same bits (a 1x1 texture, or a constant one):
+                  // bilinear() takes texel0 for its four taps instead of fetching them (same operands)
     float4 emission;
-    float4 texel0;  // a 1x1 texture's texel (RGB): bilinear() then needs no fetch
+    float4 texel0;  // the texture's first texel (RGB)
 };
 struct __align__(16) DevLight {
     float4 v0a;  // v0.xyz, area       (area light)
@@ -148,6 +149,8 @@ struct SceneView {
     float pmf;           // 1.f / (float)n_lights, Scene::sampleLight's pmf, divided on the host
     int env_tex;         // -1: BackgroundColour(0)
     int env_off, env_w, env_h;  // the environment texture (first texel, size), kernel-argument copies
+    int env_uniform;     // 1: every texel of the environment map has the same bits (env_one)
+    float env_one[3];    // its first texel
     int root_word;       // child word of the root (RTG_EXIT if no triangles)
     int root_wordw;      // root word in the wide tree
     int usew;            // wide tree available (finite bounds, children inside parents)
@@ -171,7 +174,7 @@ struct Texels4 {
     RTG_D v3 operator()(int i) const { const float4 v = t[i]; return mk(v.x, v.y, v.z); }
 };
 template <class TX>
-RTG_D v3 bilinear(TX texel, int w, int h, float tu, float tv, const float4* one = nullptr) {
+RTG_D v3 bilinear(TX texel, int w, int h, float tu, float tv, bool uni = false, v3 one = v3{0.0f, 0.0f, 0.0f}) {
     float au = fabsf(tu), av = fabsf(tv);
     float u = smax(0.0f, au) * (float)w;
     float v = smax(0.0f, av) * (float)h;
@@ -186,8 +189,8 @@ RTG_D v3 bilinear(TX texel, int w, int h, float tu, float tv, const float4* one 
     // x, y >= 0 here (u, v are >= 0 or +inf), so the modulo runs only when the coordinate wraps
     // and (x + 1) % w is a compare: same values as the reference's x % w, (x + 1) % w
     v3 s0, s1, s2, s3;
-    if (one) {  // 1x1 texture: every index wraps to texel 0, whose value the caller holds
-        s0 = s1 = s2 = s3 = mk(one->x, one->y, one->z);
+    if (uni) {  // every texel has the same bits (a 1x1 texture, or a constant one): the caller holds them
+        s0 = s1 = s2 = s3 = one;
     } else {
         x = x < w ? x : x % w;
         y = y < h ? y : y % h;
@@ -203,7 +206,7 @@ RTG_D v3 bilinear(TX texel, int w, int h, float tu, float tv, const float4* one 
 // the texels are one dependent fetch after the material record (no texinfo lookup between).
 RTG_D v3 tex_sample(const SceneView& s, const DevMat& M, float tu, float tv) {
     return bilinear(Texels4{s.texels + M.tex}, M.tex_wh & 0xffff, (int)((unsigned)M.tex_wh >> 16), tu, tv,
-                    M.tex_wh == 0x10001 ? &M.texel0 : nullptr);
+                    M.uniform != 0, mk(M.texel0.x, M.texel0.y, M.texel0.z));
 }
 
 // ------------------------------------------------------------------ division by a constant
@@ -242,7 +245,8 @@ RTG_D v3 env_eval(const SceneView& s, v3 wi) {
     u = (u < 0.0f) ? (float)((double)u + 2.0 * RTM_PI) : u;
     u = div_2pi_d(u);                // (float)((double)u / (2.0 * M_PI))
     float v = div_pi_d(rtm_acosf(wi.y));  // (float)((double)acosf(wi.y) / M_PI)
-    return bilinear(Texels4{s.texels + s.env_off}, s.env_w, s.env_h, u, v);
+    return bilinear(Texels4{s.texels + s.env_off}, s.env_w, s.env_h, u, v, s.env_uniform != 0,
+                    mk(s.env_one[0], s.env_one[1], s.env_one[2]));
 }
 RTG_D v3 background(const SceneView& s, v3 dir) {
     if (s.env_tex < 0) return mk(0.0f, 0.0f, 0.0f);  // BackgroundColour(0,0,0)::evaluate

@@ -72,6 +72,9 @@ using namespace rtgd;
 #ifndef RTG_SBVH
 #define RTG_SBVH 1          // spatial splits (rtg_bvh.hip build_sbvh); 0: object splits only
 #endif
+#ifndef RTG_UNIFORM_TEX
+#define RTG_UNIFORM_TEX 1   // constant textures of any size take the 1x1 path (no texel fetches)
+#endif
 #ifndef RTG_SBVH_BINS
 #define RTG_SBVH_BINS 32    // slabs per axis of a spatial split
 #endif
@@ -371,6 +374,8 @@ struct HostScene {
     std::vector<DevTex> texinfo;
     std::vector<float> texels;
     int n_lights = 0, env_tex = -1, env_off = 0, env_w = 1, env_h = 1;
+    bool env_uniform = false;  // every texel of the environment map has the same bits
+    float env_one[3] = {0.0f, 0.0f, 0.0f};
     int root_word = RTG_EXIT, root_wordw = RTG_EXIT;
     bool usew = false, rebuilt = false;
     uint32_t bvh_depth = 0, wide_depth = 0;

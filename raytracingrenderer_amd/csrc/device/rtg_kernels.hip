@@ -1343,12 +1343,23 @@ int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
             texels.insert(texels.end(), {t.texels[3 * j], t.texels[3 * j + 1], t.texels[3 * j + 2], 0.0f});
     }
     if (d->env_texture >= (int)d->n_textures) { g_err = "env texture out of range"; return RTG_ERR_ARG; }
+    // textures whose texels all have the same bits (1x1, or constant like C3's environment): the
+    // kernels' bilinear taps use the first texel instead of four dependent fetches (the same operands)
+    std::vector<char> uniform_tex(d->n_textures, 1);
+    for (uint32_t i = 0; i < d->n_textures; ++i) {
+        const rtg_texture& t = d->textures[i];
+        const size_t n = (size_t)t.width * t.height;
+        for (size_t j = 1; j < n && uniform_tex[i]; ++j) {
+            if (!RTG_UNIFORM_TEX) { uniform_tex[i] = 0; break; }  // (A/B: only 1x1 textures)
+            uniform_tex[i] = std::memcmp(t.texels + 3 * j, t.texels, 3 * sizeof(float)) == 0;
+        }
+    }
     for (uint32_t i = 0; i < d->n_materials; ++i) {  // texture offset and size into the material record
         const DevTex& t = texinfo[mats[i].tex];
         if (t.w > 0xffff || t.h > 0xffff) { g_err = "texture larger than 65535 texels per side"; return RTG_ERR_ARG; }
         mats[i].tex = t.off;
         mats[i].tex_wh = (int)((unsigned)t.w | ((unsigned)t.h << 16));
-        mats[i].pad = 0;
+        mats[i].uniform = uniform_tex[(size_t)(&t - texinfo.data())] ? 1 : 0;
         mats[i].texel0 = make_float4(texels[(size_t)t.off * 4], texels[(size_t)t.off * 4 + 1], texels[(size_t)t.off * 4 + 2], 0.0f);
     }
     // Identical material records merged (a scene file gives every instance its own BSDF: bathroom_f
@@ -1400,6 +1411,8 @@ int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
     hs.env_off = d->env_texture >= 0 ? hs.texinfo[d->env_texture].off : 0;
     hs.env_w = d->env_texture >= 0 ? hs.texinfo[d->env_texture].w : 1;
     hs.env_h = d->env_texture >= 0 ? hs.texinfo[d->env_texture].h : 1;
+    hs.env_uniform = d->env_texture >= 0 && uniform_tex[d->env_texture];
+    for (int k = 0; k < 3; ++k) hs.env_one[k] = d->env_texture >= 0 ? d->textures[d->env_texture].texels[k] : 0.0f;
     hs.root_word = root_word;
     hs.root_wordw = root_wordw;
     for (int k = 0; k < 6; ++k) hs.root_box[k] = d->node_bounds[k];
@@ -1460,6 +1473,8 @@ int upload_scene(int device, const HostScene& hs, rtg_handle* h) {
     s.env_off = hs.env_off;
     s.env_w = hs.env_w;
     s.env_h = hs.env_h;
+    s.env_uniform = hs.env_uniform ? 1 : 0;
+    for (int k = 0; k < 3; ++k) s.env_one[k] = hs.env_one[k];
     s.root_word = hs.root_word;
     s.nodesq = h->d_nodesq;
     s.leafbox = h->d_leafbox;
