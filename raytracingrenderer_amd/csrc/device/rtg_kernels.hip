@@ -484,7 +484,12 @@ __global__ void k_cap_slices(TraceIO io, unsigned* tab) {
 // its work distribution (8 slice counters by blockIdx % 8, 64-ray pool batches, per-lane refill).
 // Each fetch's address depends on the previous record's data (xor with `zero` = 0 at run time), so
 // every ray is one dependent chain, as in the walk. Its time is the memory system's time for this
-// exact access stream: the ceiling k_trace's time is compared against.
+// exact access stream: the ceiling k_trace's time is compared against. Between fetches
+// a chain of RTG_REPLAY_VALU dependent FMAs (round 4: 64, which the round-5 walk outran: the ceiling
+// must hold less work per fetch than the walk does).
+#ifndef RTG_REPLAY_VALU
+#define RTG_REPLAY_VALU 8
+#endif
 __global__ __launch_bounds__(RTG_TB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
 void k_replay(SceneView s, const uint4* cap, const unsigned* cap_len, const unsigned* tab, unsigned cap_n,
               unsigned zero, unsigned* fetch8, unsigned long long* total, float* out) {
@@ -557,7 +562,7 @@ void k_replay(SceneView s, const uint4* cap, const unsigned* cap_len, const unsi
                   (((nd.c.x + nd.c.y) + (nd.c.z + nd.c.w)) + __int_as_float(nd.d.x ^ nd.d.y));
         }
 #pragma unroll
-        for (int v = 0; v < 64; ++v) sum = __builtin_fmaf(sum, 1.0000001f, (float)v);
+        for (int v = 0; v < RTG_REPLAY_VALU; ++v) sum = __builtin_fmaf(sum, 1.0000001f, (float)v);
         acc += sum;
         dep = __float_as_uint(sum);
         ++fetches;

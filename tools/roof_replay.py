@@ -149,8 +149,8 @@ def main():
                       "achieved_g_fetches_per_s": achieved, "ceiling_g_fetches_per_s": ceiling,
                       "frac": achieved / ceiling,
                       "note": "ceiling = the launches' own fetch streams replayed (same addresses, per-ray order, "
-                              "ray grouping, occupancy, slice work distribution; 64 VALU/step); achieved = counted "
-                              "fetches / k_trace time of the product library"}))
+                              "ray grouping, occupancy, slice work distribution; 8 dependent VALU/step, round 4: 64); "
+                              "achieved = counted fetches / k_trace time of the product library"}))
 
 
 if __name__ == "__main__":
