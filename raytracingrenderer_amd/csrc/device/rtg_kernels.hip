@@ -544,7 +544,11 @@ void k_replay(SceneView s, const uint4* cap, const unsigned* cap_len, const unsi
         // the chain entries stream past once: non-temporal, so they do not evict the scene's lines
         // from L2 / MALL (with plain loads the replay's 16 B per 4 fetches made it slower than the
         // round-5 walk on C3 and C4)
-        if ((k & 3) == 0) q = __builtin_nontemporal_load(&cap[(size_t)(k >> 2) * cap_n + ri]);
+        if ((k & 3) == 0) {
+            typedef unsigned u4v __attribute__((ext_vector_type(4)));
+            const u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(cap) + (size_t)(k >> 2) * cap_n + ri);
+            q = make_uint4(v.x, v.y, v.z, v.w);
+        }
         const unsigned j = k & 3;
         const unsigned e = (j == 0 ? q.x : j == 1 ? q.y : j == 2 ? q.z : q.w) ^ (dep & zero);
         const unsigned type = e >> 30, idx = e & 0x3fffffffu;
