@@ -628,7 +628,7 @@ def main():
                              "tri_tail_loads_per_ray": round(cw["tri_tail_loads"] / max(all_rays, 1), 2),
                              "leafbox_tests_per_ray": round(cw["leafbox_tests"] / max(all_rays, 1), 2)},
                          "valu": valu.get("trace"),
-                         "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from an own 3-axis SAH tree over the reference leaves)",
+                         "walk": "bvh2" if a.bvh2 else "bvh4 (collapsed from an own SAH tree over the triangles with spatial splits, one triangle per leaf slot)",
                          "walk_box_tests_per_ray": round(w_nodes / max(c_ext, 1), 2),
                          "walk_tri_tests_per_ray": round(w_tris / max(c_ext, 1), 2),
                          "node_steps_per_ray": round(cw["node_lane_steps"] / max(all_rays, 1), 2),
