@@ -81,7 +81,6 @@ void k_trace(SceneView s, TraceIO io) {
     // the 8 slices (trace_slice) in LDS, read when a wave fetches work: the loop keeps only the
     // slice number in a register
     __shared__ unsigned s_tab[3][8];
-    __shared__ int s_pf[RTG_DRAIN_PF ? 64 : 1];  // drain prefetches land here (never read)
     if (tid < 8) {
         unsigned elo, elen, len;
         trace_slice(io, nc, n, tid, elo, elen, len);
@@ -345,22 +344,6 @@ void k_trace(SceneView s, TraceIO io) {
                 stk[sp + 2][tid] = wd[1];
                 sp += h;
                 cur = wd[0];
-                if (RTG_DRAIN_PF && drained) {
-                    // the drain (the work counters are dry: the memory system has spare requests):
-                    // touch the line of every pushed node or leaf triangle now, so its pop later hits
-                    // L1 / L2 instead of waiting a full fetch. 4 B per line into a per-wave LDS scratch
-                    // (global_load_lds: no VGPR is written, the compiler tracks the counter)
-                    typedef __attribute__((address_space(1))) const void* gptr_t;
-                    typedef __attribute__((address_space(3))) void* lptr_t;
-#pragma unroll
-                    for (int k = 1; k <= 3; ++k)
-                        if (k <= h) {
-                            const int w = wd[k];
-                            const void* a = w >= 0 ? (const void*)(s.nodesq + w)
-                                                   : (const void*)(tris + (~w) / RTG_LEAF_SPAN);
-                            __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)s_pf, 4, 0, 0);
-                        }
-                }
             } else {
 #pragma unroll
                 for (int k = 3; k >= 1; --k) {
