@@ -179,6 +179,11 @@ def parse():
                    help="frames of the drop-in leg (one 1-spp render call per frame, Main.cpp's loop); 0 = skip; "
                         "default 64 on C2 / C3, 0 otherwise")
     p.add_argument("--dropin-reps", type=int, default=3)
+    p.add_argument("--step-mode", default="lean", choices=["lean", "full"],
+                   help="lean: the timed steps are the renders (and exchanges) queued back to back, the ray "
+                        "counts read once after them, the per-launch HIP events in a block of steps of their "
+                        "own; full: rounds 1-5's timed step (film clear, render with per-launch events, "
+                        "stats read back, per step)")
     a = p.parse_args()
     c = CONFIGS[a.config]
     if a.steps is None:
@@ -259,8 +264,9 @@ def main():
         fx = FilmExchange(a.width, a.height, rank, world, device=coll_dev if backend == "nccl" else None)
     timing_xch = [False]
 
-    def step():
-        rt.clear()
+    def step(clear=True):
+        if clear:
+            rt.clear()
         rt.render(a.spp, tiles=tiles, first_sample=0)
         if world > 1:
             import torch
@@ -286,18 +292,24 @@ def main():
     rt.set_options(flags=base)
     for _ in range(a.warmup):
         step()
-    # timed region: per-launch HIP events on the render stream give the closest-hit kernel time
-    rt.set_options(flags=base | N.RTG_OPT_TIMING)
+    # Timed region. lean (default): the steps' renders (and at N > 1 their film exchanges) queued back
+    # to back on the device; the film is cleared once before the region (the renders add into it, as
+    # RTBase's progressive film does) and the ray counts, which accumulate since that clear, are read
+    # once after it. full (rounds 1-5): a film clear, a render with per-launch HIP events and a stats
+    # read-back per step; those host syncs and event markers cost ~1.9 % of a shard-of-8 step and
+    # ~0.5 % of C3's (profiles/r05_step_mode.txt).
+    lean = a.step_mode == "lean" and group_devs is None
+    rt.set_options(flags=base | (0 if lean else N.RTG_OPT_TIMING))
+    if lean:
+        rt.clear()
     timing_xch[0] = True
     ext_rays = shadow_rays = paths = cam_traced = chunk_spp = 0
     extend_ms = shadow_ms = shade_ms = 0.0
     extend_launches = 0
-    barrier_sync()
-    t_start = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-        st = rt.stats()
-        timed_ranks = getattr(rt, "last_ranks", None)
+    timed_ranks = None
+
+    def add_stats(st):
+        nonlocal ext_rays, cam_traced, shadow_rays, paths, extend_ms, shadow_ms, shade_ms, extend_launches, chunk_spp
         ext_rays += st["extension_rays"]
         cam_traced += st["traced_camera_rays"]
         shadow_rays += st["shadow_rays"]
@@ -307,9 +319,42 @@ def main():
         shade_ms += st["shade_ms"]
         extend_launches += st["extend_launches"]
         chunk_spp = max(chunk_spp, st.get("chunk_samples", 0))
+
+    barrier_sync()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        step(clear=not lean)
+        if not lean:
+            add_stats(rt.stats())
+            timed_ranks = getattr(rt, "last_ranks", None)
     barrier_sync()
     elapsed = time.perf_counter() - t_start
     timing_xch[0] = False
+    kernel_timing = {"source": "per-launch HIP events on the render streams, in the timed steps"}
+    if lean:
+        add_stats(rt.stats())
+        # the kernels' times: per-launch HIP events on the render streams over further steps of the
+        # same workload (renders only), scaled to the timed steps
+        rt.set_options(flags=base | N.RTG_OPT_TIMING)
+        kt = min(a.steps, 10)
+        k_ext = k_sh = k_sd = 0.0
+        k_l = 0
+        t_k = time.perf_counter()
+        for _ in range(kt):
+            rt.clear()
+            rt.render(a.spp, tiles=tiles, first_sample=0)
+            st = rt.stats()
+            k_ext += st["extend_ms"]
+            k_sh += st["shadow_ms"]
+            k_sd += st["shade_ms"]
+            k_l += st["extend_launches"]
+        t_k = time.perf_counter() - t_k
+        rt.set_options(flags=base)
+        f = a.steps / kt
+        extend_ms, shadow_ms, shade_ms, extend_launches = k_ext * f, k_sh * f, k_sd * f, int(round(k_l * f))
+        kernel_timing = {"source": "per-launch HIP events on the render streams over %d further steps of the same "
+                                   "workload (renders only), scaled to the timed steps" % kt,
+                         "steps": kt, "ms_per_step_with_events": round(t_k * 1e3 / kt, 3)}
     xch_ms = [e0.elapsed_time(e1) for e0, e1 in xch_ev]
 
     # shard-of-N projection: the exchange a rank of N adds to its render, rehearsed on this GPU (the
@@ -658,6 +703,10 @@ def main():
                                               "from profiles/, not measured in this run" % os.path.relpath(PMC_SUMMARY, ROOT))},
             "kernel_ms_per_step_rank0": {"trace": round(local_kernel_ms[0] / a.steps, 2),
                                          "generate_shade_accumulate": round(local_kernel_ms[2] / a.steps, 2)},
+            "timed_step": ("lean: renders%s queued back to back, film cleared once before, ray counts read once after"
+                           % (" + film exchanges" if world > 1 else "")) if lean else
+                          "full: film clear + render with per-launch events + stats read-back per step",
+            "kernel_timing": kernel_timing,
             "cpu_baseline": cpu,
             **({"dropin": dropin} if dropin is not None else {}),
             **({"film_reduce_bit_exact": film_check} if film_check is not None else {}),
