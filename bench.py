@@ -22,6 +22,7 @@ per chunk, and `mrays_reference_equivalent_per_s` counts it once per sample as t
   torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL via torch)
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -264,10 +265,12 @@ def main():
         fx = FilmExchange(a.width, a.height, rank, world, device=coll_dev if backend == "nccl" else None)
     timing_xch = [False]
 
+    step_stream = [None]  # lean: the timed renders and exchanges, in order on one HIP stream
+
     def step(clear=True):
         if clear:
             rt.clear()
-        rt.render(a.spp, tiles=tiles, first_sample=0)
+        rt.render(a.spp, tiles=tiles, first_sample=0, stream=step_stream[0])
         if world > 1:
             import torch
             ev = None
@@ -287,6 +290,9 @@ def main():
             torch.cuda.synchronize()
         else:
             rt.synchronize()
+            if step_stream[0]:
+                import torch
+                torch.cuda.synchronize()
 
     base = N.RTG_OPT_CULL | (N.RTG_OPT_BVH2 if a.bvh2 else 0)
     rt.set_options(flags=base)
@@ -300,8 +306,16 @@ def main():
     # ~0.5 % of C3's (profiles/r05_step_mode.txt).
     lean = a.step_mode == "lean" and group_devs is None
     rt.set_options(flags=base | (0 if lean else N.RTG_OPT_TIMING))
+    stream_ctx = contextlib.nullcontext()
     if lean:
         rt.clear()
+        # the renders are issued on a stream of their own (rtg_render_async with a stream): each is
+        # ordered after the previous step's work on it (its film exchange at N > 1) and the host does
+        # not wait between steps
+        import torch
+        s_ = torch.cuda.Stream(device=local if group_devs is None else 0)
+        step_stream[0] = s_.cuda_stream
+        stream_ctx = torch.cuda.stream(s_)
     timing_xch[0] = True
     ext_rays = shadow_rays = paths = cam_traced = chunk_spp = 0
     extend_ms = shadow_ms = shade_ms = 0.0
@@ -321,14 +335,16 @@ def main():
         chunk_spp = max(chunk_spp, st.get("chunk_samples", 0))
 
     barrier_sync()
-    t_start = time.perf_counter()
-    for _ in range(a.steps):
-        step(clear=not lean)
-        if not lean:
-            add_stats(rt.stats())
-            timed_ranks = getattr(rt, "last_ranks", None)
-    barrier_sync()
-    elapsed = time.perf_counter() - t_start
+    with stream_ctx:
+        t_start = time.perf_counter()
+        for _ in range(a.steps):
+            step(clear=not lean)
+            if not lean:
+                add_stats(rt.stats())
+                timed_ranks = getattr(rt, "last_ranks", None)
+        barrier_sync()
+        elapsed = time.perf_counter() - t_start
+    step_stream[0] = None
     timing_xch[0] = False
     kernel_timing = {"source": "per-launch HIP events on the render streams, in the timed steps"}
     if lean:

@@ -215,15 +215,20 @@ class RayTracer:
     def tiles_y(self):
         return (self.height + 31) // 32
 
-    def render(self, n_samples=1, tiles=None, first_sample=None, sync=True):
+    def render(self, n_samples=1, tiles=None, first_sample=None, sync=True, stream=None):
         """RayTracer::render(): add n_samples samples per pixel (default 1 = one frame).
         sync=False queues the frame (rtg_render_async): a frame loop of 1-spp calls then keeps up to
-        three frames in flight on the GPU; film() / stats() / synchronize() wait for them."""
+        three frames in flight on the GPU; film() / stats() / synchronize() wait for them.
+        stream (a HIP stream handle, not the null stream): the render is ordered after the caller's
+        earlier work on that stream and the caller's later work on it sees the film; the call returns
+        without waiting (rtg_render_async with a stream)."""
         first = self.getSPP() if first_sample is None else first_sample
         t = None if tiles is None else np.ascontiguousarray(tiles, np.uint32)
         tp = N.ptr(t, C.c_uint32) if t is not None else None
         nt = 0 if t is None else len(t)
-        if sync:
+        if stream:
+            rc = self._lib.rtg_render_async(self._h, first, n_samples, self.seed, tp, nt, C.c_void_p(stream))
+        elif sync:
             rc = self._lib.rtg_render(self._h, first, n_samples, self.seed, tp, nt)
         else:
             rc = self._lib.rtg_render_async(self._h, first, n_samples, self.seed, tp, nt, None)
