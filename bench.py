@@ -22,7 +22,6 @@ per chunk, and `mrays_reference_equivalent_per_s` counts it once per sample as t
   torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL via torch)
 """
 import argparse
-import contextlib
 import json
 import os
 import sys
@@ -181,10 +180,10 @@ def parse():
                         "default 64 on C2 / C3, 0 otherwise")
     p.add_argument("--dropin-reps", type=int, default=3)
     p.add_argument("--step-mode", default="lean", choices=["lean", "full"],
-                   help="lean: the timed steps are the renders (and exchanges) queued back to back, the ray "
-                        "counts read once after them, the per-launch HIP events in a block of steps of their "
-                        "own; full: rounds 1-5's timed step (film clear, render with per-launch events, "
-                        "stats read back, per step)")
+                   help="lean: the timed steps are queued renders (rtg_render_async: consecutive frames overlap "
+                        "in the frame pipeline) and their film exchanges, the ray counts read once after them, "
+                        "the per-launch HIP events in a block of steps of their own; full: rounds 1-5's timed "
+                        "step (film clear, a waited-for render with per-launch events, stats read back, per step)")
     a = p.parse_args()
     c = CONFIGS[a.config]
     if a.steps is None:
@@ -265,12 +264,15 @@ def main():
         fx = FilmExchange(a.width, a.height, rank, world, device=coll_dev if backend == "nccl" else None)
     timing_xch = [False]
 
-    step_stream = [None]  # lean: the timed renders and exchanges, in order on one HIP stream
+    queued = [False]  # lean timed steps: queued renders
 
     def step(clear=True):
         if clear:
             rt.clear()
-        rt.render(a.spp, tiles=tiles, first_sample=0, stream=step_stream[0])
+        if queued[0]:
+            rt.render(a.spp, tiles=tiles, first_sample=0, sync=False)
+        else:
+            rt.render(a.spp, tiles=tiles, first_sample=0)
         if world > 1:
             import torch
             ev = None
@@ -290,9 +292,6 @@ def main():
             torch.cuda.synchronize()
         else:
             rt.synchronize()
-            if step_stream[0]:
-                import torch
-                torch.cuda.synchronize()
 
     base = N.RTG_OPT_CULL | (N.RTG_OPT_BVH2 if a.bvh2 else 0)
     rt.set_options(flags=base)
@@ -306,16 +305,12 @@ def main():
     # ~0.5 % of C3's (profiles/r05_step_mode.txt).
     lean = a.step_mode == "lean" and group_devs is None
     rt.set_options(flags=base | (0 if lean else N.RTG_OPT_TIMING))
-    stream_ctx = contextlib.nullcontext()
     if lean:
         rt.clear()
-        # the renders are issued on a stream of their own (rtg_render_async with a stream): each is
-        # ordered after the previous step's work on it (its film exchange at N > 1) and the host does
-        # not wait between steps
-        import torch
-        s_ = torch.cuda.Stream(device=local if group_devs is None else 0)
-        step_stream[0] = s_.cuda_stream
-        stream_ctx = torch.cuda.stream(s_)
+        # each step's render is queued (rtg_render_async): the host does not wait, and a render of
+        # up to 16M paths runs in the frame pipeline, its traversal starting while the frame before
+        # it drains (its film fold still after that frame's fold and film exchange)
+        queued[0] = True
     timing_xch[0] = True
     ext_rays = shadow_rays = paths = cam_traced = chunk_spp = 0
     extend_ms = shadow_ms = shade_ms = 0.0
@@ -335,16 +330,15 @@ def main():
         chunk_spp = max(chunk_spp, st.get("chunk_samples", 0))
 
     barrier_sync()
-    with stream_ctx:
-        t_start = time.perf_counter()
-        for _ in range(a.steps):
-            step(clear=not lean)
-            if not lean:
-                add_stats(rt.stats())
-                timed_ranks = getattr(rt, "last_ranks", None)
-        barrier_sync()
-        elapsed = time.perf_counter() - t_start
-    step_stream[0] = None
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        step(clear=not lean)
+        if not lean:
+            add_stats(rt.stats())
+            timed_ranks = getattr(rt, "last_ranks", None)
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
+    queued[0] = False
     timing_xch[0] = False
     kernel_timing = {"source": "per-launch HIP events on the render streams, in the timed steps"}
     if lean:
@@ -719,8 +713,8 @@ def main():
                                               "from profiles/, not measured in this run" % os.path.relpath(PMC_SUMMARY, ROOT))},
             "kernel_ms_per_step_rank0": {"trace": round(local_kernel_ms[0] / a.steps, 2),
                                          "generate_shade_accumulate": round(local_kernel_ms[2] / a.steps, 2)},
-            "timed_step": ("lean: renders%s queued back to back, film cleared once before, ray counts read once after"
-                           % (" + film exchanges" if world > 1 else "")) if lean else
+            "timed_step": ("lean: queued renders (frame pipeline)%s, film cleared once before, ray counts read once "
+                           "after" % (" + film exchanges" if world > 1 else "")) if lean else
                           "full: film clear + render with per-launch events + stats read-back per step",
             "kernel_timing": kernel_timing,
             "cpu_baseline": cpu,

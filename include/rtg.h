@@ -190,7 +190,9 @@ int  rtg_set_integrator(rtg_handle* h, int integrator);
  *     once). Issued work of at most 16M paths per chunk runs in a pipeline of 3 slots, each with its
  *     own path state and stream, with no host wait: chunks run side by side on the GPU, a call waits
  *     only for the chunk three before it to leave the GPU, and the film updates stay in sample
- *     order, so the film is bit-identical to one rtg_render of all the samples. Larger chunks (the
+ *     order, so the film is bit-identical to one rtg_render of all the samples. A pipelined chunk's
+ *     traversal may start before the caller's earlier film reads on the handle (rtg_film_gather,
+ *     ...) have run; only its film fold waits for them. Larger chunks (the
  *     call that reaches the 64M threshold issues one) read each bounce's live count back during the
  *     traversal, so that call returns once the chunk's last bounce is issued; the calls before it
  *     return at once. rtg_film_read with a film pointer,
@@ -277,7 +279,8 @@ int  rtg_group_setup_ms(rtg_group* g, double* prepare_ms, double* upload_ms);  /
  * order rtg_film_gather packs them: tile by tile, row-major inside a tile, clipped at the film
  * edge (pixels NULL: only the count). rtg_film_gather copies the handle's film pixels listed in
  * pixels_dev (device array of n indices; 0xFFFFFFFF = padding, packed as zeros) to dst_dev (3n
- * floats), ordered after every render queued on the handle; rtg_film_scatter writes src_dev's n
+ * floats), ordered after every render queued on the handle, and the handle's later film writes
+ * (the folds of renders queued after it) wait for it; rtg_film_scatter writes src_dev's n
  * packed pixels into film_dev (width * height * 3 floats) at the listed indices (0xFFFFFFFF:
  * skipped). Both run on hip_stream (NULL: the handle's stream / the device's null stream) and
  * return without waiting. */

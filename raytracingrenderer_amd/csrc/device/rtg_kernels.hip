@@ -1792,7 +1792,11 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         const hipStream_t ss = sl.stream;
         PathBufs& pb = sl.pb;
         io.ovf = sl.d_ovf;
-        HIPOK(hipStreamWaitEvent(ss, h->entry, 0));
+        // A chunk starts after the caller's earlier work on st. A queued (pipelined) chunk reads
+        // nothing the caller's work on the handle's stream writes (film reads and gathers, film
+        // loads; pixel lists and clears wait for the device on the host), so only its fold waits
+        // for that work, below: the chunk's traversal can start while earlier frames drain.
+        if (!pipe) HIPOK(hipStreamWaitEvent(ss, h->entry, 0));
         if (RTG_DEBUG && h->wavetime && c == 0) {
             HIPOK(hipMalloc((void**)&d_wt, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long)));
             HIPOK(hipMemsetAsync(d_wt, 0, (size_t)(maxb + 1) * wt_waves * 3 * sizeof(unsigned long long), ss));
@@ -1911,6 +1915,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         // the film takes the chunks in sample order: this fold runs after the previous chunk's
         RoctxRange r_acc("rtg:accumulate");
         if (h->last_fold) HIPOK(hipStreamWaitEvent(ss, h->last_fold, 0));
+        if (pipe) HIPOK(hipStreamWaitEvent(ss, h->entry, 0));  // the film's readers and writers so far
         timed_begin(h, ss, k);
         if (a.ns > 1) {
             const unsigned ppw = a.ns <= 32 ? 64u / (a.ns < 4 ? 4u : a.ns) : 1u;  // pixels per wave (k_accumulate_pm)

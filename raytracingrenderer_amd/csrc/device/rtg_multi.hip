@@ -216,6 +216,12 @@ int rtg_film_gather(rtg_handle* h, const uint32_t* pixels_dev, uint32_t n, float
         hipLaunchKernelGGL(k_film_gather, dim3((n + 255) / 256), dim3(256), 0, st, (const float*)h->d_film, pixels_dev, n,
                            dst_dev);
         LAUNCH_OK("k_film_gather");
+        if (st != h->stream) {
+            // the handle's later film writes (the next renders' folds wait on its stream) come after
+            // this read of the film
+            HIPOK(hipEventRecord(h->ev[3], st));
+            HIPOK(hipStreamWaitEvent(h->stream, h->ev[3], 0));
+        }
     }
     return RTG_OK;
 }

@@ -67,8 +67,22 @@ class FilmExchange:
         self.t_all = torch.from_numpy(self.all.view(np.int32)).to(dev) if rank == 0 else None
         self.pack = torch.zeros(self.maxpix * 3, dtype=torch.float32, device=dev)
         self.recv = torch.zeros((world, self.maxpix * 3), dtype=torch.float32, device=dev) if rank == 0 else None
+        # CUDA: the exchange runs on a stream of its own (never the null stream, which librtg would
+        # take for the handle's), after the caller's earlier work; the caller's later work waits for it
+        self.stream = torch.cuda.Stream(device=dev) if self.cuda else None
 
     def exchange(self, rt, film_tensor, dist):
+        import torch
+        if not self.cuda:
+            return self._exchange(rt, film_tensor, dist)
+        cur = torch.cuda.current_stream(self.stream.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self._exchange(rt, film_tensor, dist)
+        cur.wait_stream(self.stream)
+        return film_tensor
+
+    def _exchange(self, rt, film_tensor, dist):
         import torch
         from raytracingrenderer_amd import _native as N
         if self.cuda:
