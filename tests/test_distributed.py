@@ -201,6 +201,36 @@ def test_device_gather_scatter_assemble_one_render(world):
     assert np.array_equal(film.cpu().numpy().view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.gpu
+def test_pipelined_frames_exchange_sees_each_frame():
+    """bench.py's lean step at N > 1: queued renders (the frame pipeline: a frame's traversal starts
+    while the previous frame drains) each followed by FilmExchange on its own stream, with no host
+    wait in between. The exchange of step k must read exactly the film after frame k (the fold of
+    frame k + 1 waits for it): every assembled snapshot equals the film a waited-for render loop
+    reads after the same frame, bit for bit."""
+    import torch
+    from raytracingrenderer_amd import RayTracer, loadScene
+    from raytracingrenderer_amd.distributed import FilmExchange
+    W, H = 160, 128  # 20480 pixels x 16 spp: a 328k-path frame, inside the pipeline's chunk limit
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=W, height=H)
+    ref = RayTracer(s, seed=21)
+    want = []
+    for k in range(4):
+        ref.render(16, first_sample=16 * k)
+        want.append(ref.film()[0])
+    rt = RayTracer(s, seed=21)
+    fx = FilmExchange(W, H, 0, 1, device="cuda:0")
+    film = torch.full((H, W, 3), float("nan"), dtype=torch.float32, device="cuda:0")
+    snaps = []
+    for k in range(4):
+        rt.render(16, first_sample=16 * k, sync=False)
+        fx.exchange(rt, film, None)
+        snaps.append(film.clone())  # on the caller's stream, after the exchange
+    torch.cuda.synchronize()
+    for k in range(4):
+        assert np.array_equal(snaps[k].cpu().numpy().view(np.uint32), want[k].view(np.uint32)), k
+
+
 def test_native_tile_partition_matches_python():
     """rtg_tiles_for_rank (librtg, used by rtg_group and the CLI's -gpus) is the partition of
     distributed.tiles_for_rank (pure host code: no GPU needed)."""
