@@ -296,6 +296,35 @@ def test_queued_frames_past_the_coalescing_threshold(cornell256):
     assert rt.stats()["paths"] == n * 256 * 256
 
 
+def test_queued_frames_then_user_stream_renders_then_reads(tmp_path):
+    """Queued frames (rtg_render_async, no stream), then renders on a user HIP stream (rtg_render_async
+    with a stream: no host wait, not the handle's stream), then reads: the film read and the stats
+    wait for the queued chunks and the stream's renders alike, and the film equals one waited-for
+    render of all the samples. A clear after such a mix leaves nothing to fold later."""
+    import torch
+    d = str(tmp_path / "s")
+    write_synthetic_scene(d, n_tris=200000, seed=5, width=512, height=512)
+    s = loadScene(d)
+    full = gpu_film(s, 8, seed=41)
+    rt = RayTracer(s, seed=41)
+    us = torch.cuda.Stream()
+    for f in range(4):
+        rt.render(1, first_sample=f, sync=False)
+    for f in range(4, 8):
+        rt.render(1, first_sample=f, stream=us.cuda_stream)
+    film, spp = rt.film()
+    assert spp == 8
+    assert_bitexact(film, full, "4 queued frames + 4 frames on a user stream vs one 8-spp render")
+    assert rt.stats()["paths"] == 8 * 512 * 512
+    for f in range(3):
+        rt.render(1, first_sample=f, sync=False)
+    rt.render(1, first_sample=3, stream=us.cuda_stream)
+    rt.clear()
+    torch.cuda.synchronize()
+    film2, spp2 = rt.film()
+    assert spp2 == 0 and not film2.any()
+
+
 @pytest.mark.parametrize("name", ["cornell256", "synth20k"])
 @pytest.mark.parametrize("cull", [True, False])
 def test_ray_queries_match_reference(name, cull, cornell256, synth20k):
