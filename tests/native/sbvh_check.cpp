@@ -33,10 +33,16 @@ int main(int argc, char** argv) {
     std::vector<std::vector<int>> frags(d->n_tris);
     std::vector<int> stack{0}, depth(nn, 0);
     size_t leaves = 0, maxd = 0, bad = 0;
+    auto area = [&](int n) {
+        const double x = bd[n * 6 + 3] - bd[n * 6], y = bd[n * 6 + 4] - bd[n * 6 + 1], z = bd[n * 6 + 5] - bd[n * 6 + 2];
+        return x * y + y * z + z * x;
+    };
+    double sa_int = 0.0, sa_leaf = 0.0;  // summed surface areas / the root's (the SAH's two terms)
     while (!stack.empty()) {
         const int n = stack.back();
         stack.pop_back();
         maxd = std::max(maxd, (size_t)depth[n]);
+        (lk[n * 4] < 0 ? sa_leaf : sa_int) += area(n) / area(0);
         if (lk[n * 4] < 0) {
             ++leaves;
             frags[lk[n * 4 + 2]].push_back(n);
@@ -71,7 +77,8 @@ int main(int argc, char** argv) {
         }
     }
     std::printf("tris %u nodes %zu leaves %zu (dup %.3f) depth %zu build %.0f ms | bad boxes %zu, missing tris %zu, "
-                "uncovered points %zu\n", d->n_tris, nn, leaves, (double)leaves / d->n_tris, maxd, ms, bad, missing, uncovered);
+                "uncovered points %zu | area sums / root: internal %.2f leaves %.2f\n", d->n_tris, nn, leaves,
+                (double)leaves / d->n_tris, maxd, ms, bad, missing, uncovered, sa_int, sa_leaf);
     rth_free_scene(s);
     return (bad || missing || uncovered) ? 1 : 0;
 }
