@@ -274,14 +274,10 @@ def main():
         else:
             rt.render(a.spp, tiles=tiles, first_sample=0)
         if world > 1:
-            import torch
-            ev = None
-            if backend == "nccl" and timing_xch[0]:
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                ev[0].record()
-            fx.exchange(rt, film_t, dist)  # own tiles -> rank 0 (pack, RCCL gather, scatter)
+            # own tiles -> rank 0 (pack, RCCL gather, scatter); timed with CUDA events on the exchange's
+            # stream from the moment the frame is on the film (not while the queued render runs)
+            ev = fx.exchange(rt, film_t, dist, timing=backend == "nccl" and timing_xch[0])
             if ev is not None:
-                ev[1].record()
                 xch_ev.append(ev)
 
     def barrier_sync():
@@ -723,7 +719,7 @@ def main():
             **({"exchange_ms_per_step": {"mean": round(float(np.mean(xch_ms)), 3), "max": round(float(np.max(xch_ms)), 3),
                                          "bytes_per_rank": fx.maxpix * 12,
                                          "what": "rank %d: own-tile pack + RCCL gather to rank 0 + scatter (CUDA events "
-                                                 "on the current stream)" % rank}}
+                                                 "on the exchange stream, from the frame's fold to the scatter)" % rank}}
                if xch_ms else {}),
             **({"shard_exchange": shard_exchange} if shard_exchange is not None else {}),
             **({"group": group_info} if group_info is not None else {}),

@@ -71,16 +71,31 @@ class FilmExchange:
         # take for the handle's), after the caller's earlier work; the caller's later work waits for it
         self.stream = torch.cuda.Stream(device=dev) if self.cuda else None
 
-    def exchange(self, rt, film_tensor, dist):
+    def exchange(self, rt, film_tensor, dist, timing=False):
+        """Assemble film_tensor on rank 0. timing=True (CUDA): returns (start, end) CUDA events on the
+        exchange's stream, start recorded once the rank's queued frames are on its film (so the pair
+        times the exchange alone); otherwise returns None."""
         import torch
+        from raytracingrenderer_amd import _native as N
         if not self.cuda:
-            return self._exchange(rt, film_tensor, dist)
+            self._exchange(rt, film_tensor, dist)
+            return None
         cur = torch.cuda.current_stream(self.stream.device)
         self.stream.wait_stream(cur)
+        ev = None
         with torch.cuda.stream(self.stream):
+            if timing:
+                # rtg_film_gather of no pixels: only the wait for the handle's frames
+                rc = N.rtg().rtg_film_gather(rt.handle, None, 0, None, C.c_void_p(self.stream.cuda_stream))
+                if rc:
+                    raise RuntimeError(N.rtg().rtg_last_error().decode())
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(self.stream)
             self._exchange(rt, film_tensor, dist)
+            if timing:
+                ev[1].record(self.stream)
         cur.wait_stream(self.stream)
-        return film_tensor
+        return ev
 
     def _exchange(self, rt, film_tensor, dist):
         import torch
@@ -144,4 +159,5 @@ def render_sharded(rt, n_samples, rank, world, dist=None, film_tensor=None, firs
         return film_tensor
     if exchange is None:
         exchange = FilmExchange(rt.width, rt.height, rank, world, film_tensor.device if film_tensor.is_cuda else None)
-    return exchange.exchange(rt, film_tensor, dist)
+    exchange.exchange(rt, film_tensor, dist)
+    return film_tensor

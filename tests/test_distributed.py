@@ -221,12 +221,15 @@ def test_pipelined_frames_exchange_sees_each_frame():
     rt = RayTracer(s, seed=21)
     fx = FilmExchange(W, H, 0, 1, device="cuda:0")
     film = torch.full((H, W, 3), float("nan"), dtype=torch.float32, device="cuda:0")
-    snaps = []
+    snaps, evs = [], []
     for k in range(4):
         rt.render(16, first_sample=16 * k, sync=False)
-        fx.exchange(rt, film, None)
+        ev = fx.exchange(rt, film, None, timing=k >= 2)  # timed: start once the frame is on the film
+        if ev is not None:
+            evs.append(ev)
         snaps.append(film.clone())  # on the caller's stream, after the exchange
     torch.cuda.synchronize()
+    assert len(evs) == 2 and all(0.0 <= e0.elapsed_time(e1) < 50.0 for e0, e1 in evs)
     for k in range(4):
         assert np.array_equal(snaps[k].cpu().numpy().view(np.uint32), want[k].view(np.uint32)), k
 
