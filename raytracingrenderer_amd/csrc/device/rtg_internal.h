@@ -72,9 +72,6 @@ using namespace rtgd;
 #ifndef RTG_SBVH
 #define RTG_SBVH 1          // spatial splits (rtg_bvh.hip build_sbvh); 0: object splits only
 #endif
-#ifndef RTG_SHADOW_HOLD
-#define RTG_SHADOW_HOLD 0   // 1: a shadow ray with a parked leaf waits for the leaf phase (A/B)
-#endif
 #ifndef RTG_UNIFORM_TEX
 #define RTG_UNIFORM_TEX 1   // constant textures of any size take the 1x1 path (no texel fetches)
 #endif

@@ -255,10 +255,7 @@ void k_trace(SceneView s, TraceIO io) {
             }
         };
         // ---- one traversal step
-        // RTG_SHADOW_HOLD: a shadow ray with a parked leaf waits for the leaf phase (its triangle may
-        // end the ray) instead of walking on
-        const bool held = RTG_SHADOW_HOLD && anyr && pend != RTG_EXIT;
-        if (cur >= 0 && wide && !held) {
+        if (cur >= 0 && wide) {
             int wd[4];
             float key[4];
             {
@@ -359,7 +356,7 @@ void k_trace(SceneView s, TraceIO io) {
                 }
                 cur = wd[0];
             }
-        } else if (cur >= 0 && !held) {
+        } else if (cur >= 0) {
             if (COUNT) (anyr ? c_snodes : c_nodes) += 2;
             capture(3u, (unsigned)cur);
             const DevNode nd = s.nodes[cur];
@@ -409,8 +406,7 @@ void k_trace(SceneView s, TraceIO io) {
         // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on, or (the queue is
         // dry) any parked leaf: the drain is latency-bound, lanes should not wait for each other
         const unsigned long long pm = __ballot(pend != RTG_EXIT);
-        if (__popcll(pm) >= RTG_POSTPONE ||
-            __ballot(cur >= 0 && !(RTG_SHADOW_HOLD && anyr && pend != RTG_EXIT)) == 0 || (drained && pm)) {
+        if (__popcll(pm) >= RTG_POSTPONE || __ballot(cur >= 0) == 0 || (drained && pm)) {
             if (COUNT) {
                 c_lslots += 64;
                 c_lstep += pend != RTG_EXIT ? 1 : 0;
