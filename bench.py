@@ -107,8 +107,10 @@ def scene_dir(name):
 class GroupRender:
     """The native one-process group (RayTracerGroup: rtg_group_* in rtg_multi.hip) behind the calls
     bench.py makes on a RayTracer: render = every rank renders its diagonal tile stripes on its own
-    device (one host thread each), then the own-tile film exchange into devices[0]; stats are summed over
-    the ranks."""
+    device, then the own-tile film exchange into devices[0]; stats are summed over the ranks. sync=False
+    (the lean timed step) queues both: rtg_group_render_async (every rank's frame in its frame
+    pipeline) and rtg_group_reduce_async (the exchange on its own streams, after each rank's frame),
+    with no host wait; synchronize() waits for the ranks and the exchanges."""
 
     def __init__(self, scene, devices, max_depth, max_paths):
         from raytracingrenderer_amd import RayTracerGroup
@@ -125,13 +127,14 @@ class GroupRender:
     def clear(self):
         self.g.clear()
 
-    def render(self, spp, tiles=None, first_sample=0):
-        self.g.render(spp, first_sample=first_sample)  # synchronous per rank
-        self.g.reduce()
-        self.reduce_ms.append(self.g.reduce_ms())
+    def render(self, spp, tiles=None, first_sample=0, sync=True):
+        self.g.render(spp, first_sample=first_sample, sync=sync)
+        self.g.reduce(sync=sync)
+        if sync:
+            self.reduce_ms.append(self.g.reduce_ms())
 
     def synchronize(self):
-        pass  # group calls return when their devices are done
+        self.g.synchronize()
 
     def stats(self):
         self.last_ranks = self.g.rank_stats()
@@ -299,13 +302,14 @@ def main():
     # once after it. full (rounds 1-5): a film clear, a render with per-launch HIP events and a stats
     # read-back per step; those host syncs and event markers cost ~1.9 % of a shard-of-8 step and
     # ~0.5 % of C3's (profiles/r05_step_mode.txt).
-    lean = a.step_mode == "lean" and group_devs is None
+    lean = a.step_mode == "lean"
     rt.set_options(flags=base | (0 if lean else N.RTG_OPT_TIMING))
     if lean:
         rt.clear()
-        # each step's render is queued (rtg_render_async): the host does not wait, and a render of
-        # up to 16M paths runs in the frame pipeline, its traversal starting while the frame before
-        # it drains (its film fold still after that frame's fold and film exchange)
+        # each step's render is queued (rtg_render_async; the native group: rtg_group_render_async +
+        # rtg_group_reduce_async): the host does not wait, and a render of up to 16M paths runs in the
+        # frame pipeline, its traversal starting while the frame before it drains (its film fold
+        # still after that frame's fold and film exchange)
         queued[0] = True
     timing_xch[0] = True
     ext_rays = shadow_rays = paths = cam_traced = chunk_spp = 0
@@ -355,6 +359,7 @@ def main():
             k_sd += st["shade_ms"]
             k_l += st["extend_launches"]
         t_k = time.perf_counter() - t_k
+        timed_ranks = getattr(rt, "last_ranks", None)
         rt.set_options(flags=base)
         f = a.steps / kt
         extend_ms, shadow_ms, shade_ms, extend_launches = k_ext * f, k_sh * f, k_sd * f, int(round(k_l * f))
@@ -390,8 +395,10 @@ def main():
     film_check = None
     group_reduced = None
     if group_devs is not None and a.verify_film:
+        # the lean step's path: two queued frames, each followed by a queued exchange
         rt.clear()
-        rt.render(a.spp, first_sample=0)
+        for _ in range(2):
+            rt.render(a.spp, first_sample=0, sync=False)
         group_reduced = rt.film()[0]  # checked against one handle once the group is released
     if world > 1 and a.verify_film:
         step()  # a fresh reduced film
@@ -410,7 +417,8 @@ def main():
         r0 = timed_ranks[0] if timed_ranks else {}
         local_kernel_ms = (r0.get("extend_ms", 0.0) * a.steps, 0.0, r0.get("shade_ms", 0.0) * a.steps)
         prep_ms, up_ms = rt.g.setup_ms()
-        timed_reduce = rt.reduce_ms[a.warmup:a.warmup + a.steps]
+        # waited-for exchanges: the timed steps' (full), or the kernel-timing steps' after them (lean)
+        timed_reduce = rt.reduce_ms[-min(a.steps, 10):] if lean else rt.reduce_ms[a.warmup:a.warmup + a.steps]
         group_info = {"devices": group_devs, "distinct_gpus": len(set(group_devs)), "uses_rccl": rt.g.uses_rccl,
                       "setup_ms": {"create_total": round(rt.create_s * 1e3, 1), "host_build": round(prep_ms, 1),
                                    "parallel_uploads": round(up_ms, 1)},
@@ -435,7 +443,8 @@ def main():
             import gc
             gc.collect()
             solo = RayTracer(scene, device=group_devs[0], max_depth=a.max_depth, seed=1234, max_paths=a.max_paths)
-            solo.render(a.spp, first_sample=0)
+            for _ in range(2):
+                solo.render(a.spp, first_sample=0)
             film_check = bool(np.array_equal(group_reduced.view(np.uint32), solo.film()[0].view(np.uint32)))
             del solo
     # rays traced: renderTile's camera ray is the pixel centre's for every sample (Renderer.h:805-808),
@@ -608,9 +617,11 @@ def main():
                        "triangles": scene.desc.n_tris, "width": a.width, "height": a.height, "spp": a.spp,
                        "chunk_spp": chunk_spp,
                        "max_depth": a.max_depth,
-                       "parallelism": ("tile-sharded x%d + own-tile film exchange over %s" % (world, "RCCL" if backend == "nccl" else backend)
-                                       if group_devs is None else
-                                       group_parallelism)},
+                       "parallelism": (group_parallelism if group_devs is not None else
+                                       "tile-sharded x%d (torchrun ranks) + own-tile film exchange over %s"
+                                       % (world, "RCCL" if backend == "nccl" else backend) if world > 1 else
+                                       "one GPU rendering rank 0's tiles of %d (shard-of diagnostic, no exchange)" % a.shard_of
+                                       if a.shard_of > 1 else "one GPU, every tile (no exchange)")},
             # headline roofline: a hardware peak. SURVEY.md 8d's algorithmic bytes of k_trace per
             # launch / its average launch time, against the L2 aggregate bandwidth that serves them
             # (they exceed the HBM peak: the ~70 MB hot scene lives in L2 + Infinity Cache, and the
@@ -714,6 +725,14 @@ def main():
                           "full: film clear + render with per-launch events + stats read-back per step",
             "kernel_timing": kernel_timing,
             "cpu_baseline": cpu,
+            # one unit on both sides: the CPU's rays are the reference's (a camera ray per sample), so
+            # they compare with mrays_reference_equivalent_per_s, not with `value` (traced rays); and
+            # ms per 1-spp frame of the same film
+            **({"gpu_over_cpu": {"ms_per_frame": round(cpu["ms_per_frame"] / (ms_step / a.spp), 1),
+                                 "reference_equivalent_mrays": round(mrays / cpu["value"], 1),
+                                 "note": "CPU: %d host threads (cores); same scene, film size and MAX_DEPTH"
+                                         % cpu["cores"]}}
+               if cpu and cpu.get("value") and cpu.get("ms_per_frame") else {}),
             **({"dropin": dropin} if dropin is not None else {}),
             **({"film_reduce_bit_exact": film_check} if film_check is not None else {}),
             **({"exchange_ms_per_step": {"mean": round(float(np.mean(xch_ms)), 3), "max": round(float(np.max(xch_ms)), 3),
@@ -810,7 +829,7 @@ def rehearse_exchange(rt, a, reps=20):
     g_ms = timed(lambda: N.rtg().rtg_film_gather(rt.handle, C.c_void_p(fx.t_own.data_ptr()), fx.maxpix,
                                                    C.c_void_p(fx.recv[0].data_ptr()), stream))
     s_ms = timed(lambda: N.rtg().rtg_film_scatter(0, C.c_void_p(fx.recv.data_ptr()), C.c_void_p(fx.t_all.data_ptr()),
-                                                    len(fx.all), C.c_void_p(film.data_ptr()), stream))
+                                                    len(fx.all), C.c_void_p(film.data_ptr()), a.width * a.height, stream))
     msg = fx.maxpix * 12
     x_ms = (msg / (XGMI_LINK_GBS * 1e9)) * 1e3 + RCCL_P2P_US / 1e3
     return {"ranks": n, "bytes_per_rank": msg, "gather_ms": round(g_ms, 4), "scatter_ms": round(s_ms, 4),
@@ -894,7 +913,7 @@ def cpu_baseline(scene, a, scene_path=None):
         if time.perf_counter() - t0 > a.cpu_seconds:
             break
     dt = time.perf_counter() - t0
-    return dict(base, value=round(rays / dt / 1e6, 3), unit="Mray/s", kind=kind,
+    return dict(base, value=round(rays / dt / 1e6, 3), unit="Mray/s (reference rays: a camera ray per sample)", kind=kind,
                 sample="%d full %dx%d frame(s) at 1 spp of the same scene, MAX_DEPTH %d (%d paths, %d rays) in "
                        "%.1f s; %s; glibc math" % (frames, scene.width, scene.height, a.max_depth, paths, rays, dt, what),
                 ms_per_frame=round(dt * 1e3 / frames, 1), mpaths_per_s=round(paths / dt / 1e6, 3),

@@ -35,8 +35,10 @@ extern "C" {
  * 4: rtg_render_async queues frames (returns before any of its work has run), rtg_render_idle,
  *    rtg_stats.traced_camera_rays appended;
  * 5: rtg_build_id; the own-tile film exchange (rtg_tile_pixels, rtg_film_gather, rtg_film_scatter),
- *    which rtg_group_reduce now uses in place of a whole-film ncclReduce; rtg_stats.chunk_samples */
-#define RTG_ABI_VERSION 5
+ *    which rtg_group_reduce now uses in place of a whole-film ncclReduce; rtg_stats.chunk_samples
+ * 6: rtg_group_render_async / rtg_group_reduce_async / rtg_group_synchronize (queued group frames);
+ *    rtg_film_scatter takes the film's pixel count */
+#define RTG_ABI_VERSION 6
 
 /* error codes */
 #define RTG_OK              0
@@ -267,9 +269,19 @@ rtg_handle* rtg_group_handle(rtg_group* g, int rank);  /* e.g. for rtg_get_stats
 int  rtg_group_set_options(rtg_group* g, int max_depth, int flags, uint32_t max_paths);
 int  rtg_group_render(rtg_group* g, uint32_t first_sample, uint32_t n_samples, uint64_t seed);
 int  rtg_group_reduce(rtg_group* g);  /* the films stay per device; the assembled film goes to a separate buffer */
+/* Queued forms (the frame loop of Main.cpp:74-118 on N devices). rtg_group_render_async is every
+ * rank's rtg_render_async (NULL stream) on its device: frames are coalesced and pipelined per rank
+ * as on one handle, and the call returns without waiting for the GPUs. rtg_group_reduce_async
+ * queues the own-tile exchange on per-rank exchange streams after each rank's queued frames (pack,
+ * RCCL send/recv, scatter on devices[0]); the ranks' next frames start their traversal meanwhile
+ * and only their film folds wait for the packs. rtg_group_synchronize waits for both;
+ * rtg_group_film_read waits for the exchange it reads. */
+int  rtg_group_render_async(rtg_group* g, uint32_t first_sample, uint32_t n_samples, uint64_t seed);
+int  rtg_group_reduce_async(rtg_group* g);
+int  rtg_group_synchronize(rtg_group* g);
 int  rtg_group_film_read(rtg_group* g, float* rgb_sum /* width*height*3 */, uint32_t* spp);  /* reduces if needed */
 int  rtg_group_clear(rtg_group* g);
-double rtg_group_reduce_ms(rtg_group* g);  /* device time of the last reduce */
+double rtg_group_reduce_ms(rtg_group* g);  /* device time of the last reduce (set when the group is synchronized) */
 int  rtg_group_uses_rccl(rtg_group* g);    /* 1: RCCL communicator, 0: host-memory sum (repeated devices) */
 int  rtg_group_setup_ms(rtg_group* g, double* prepare_ms, double* upload_ms);  /* host build, parallel uploads */
 
@@ -281,14 +293,15 @@ int  rtg_group_setup_ms(rtg_group* g, double* prepare_ms, double* upload_ms);  /
  * pixels_dev (device array of n indices; 0xFFFFFFFF = padding, packed as zeros) to dst_dev (3n
  * floats), ordered after every render queued on the handle, and the handle's later film writes
  * (the folds of renders queued after it) wait for it; rtg_film_scatter writes src_dev's n
- * packed pixels into film_dev (width * height * 3 floats) at the listed indices (0xFFFFFFFF:
- * skipped). Both run on hip_stream (NULL: the handle's stream / the device's null stream) and
+ * packed pixels into film_dev (film_pixels * 3 floats) at the listed indices (0xFFFFFFFF:
+ * skipped). An index at or past the film's pixel count is treated as padding by both (never
+ * read or written). Both run on hip_stream (NULL: the handle's stream / the device's null stream) and
  * return without waiting. */
 int  rtg_tile_pixels(uint32_t width, uint32_t height, const uint32_t* tile_ids, uint32_t n_tiles,
                      uint32_t* pixels /* or NULL */, uint32_t* n_pixels);
 int  rtg_film_gather(rtg_handle* h, const uint32_t* pixels_dev, uint32_t n, float* dst_dev, void* hip_stream);
 int  rtg_film_scatter(int device, const float* src_dev, const uint32_t* pixels_dev, uint32_t n, float* film_dev,
-                      void* hip_stream);
+                      uint32_t film_pixels /* width * height of film_dev */, void* hip_stream);
 
 /* Film access: the unnormalised sum (Film::film) and the sample count (Film::SPP). */
 int  rtg_film_read(rtg_handle* h, float* rgb_sum /* width*height*3 */, uint32_t* spp);

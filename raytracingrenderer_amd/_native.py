@@ -110,6 +110,9 @@ RTG_EXPORTS = [
     ("rtg_group_set_options", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_uint32]),
     ("rtg_group_render", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64]),
     ("rtg_group_reduce", C.c_int, [C.c_void_p]),
+    ("rtg_group_render_async", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64]),
+    ("rtg_group_reduce_async", C.c_int, [C.c_void_p]),
+    ("rtg_group_synchronize", C.c_int, [C.c_void_p]),
     ("rtg_group_film_read", C.c_int, [C.c_void_p, f32p, u32p]),
     ("rtg_group_clear", C.c_int, [C.c_void_p]),
     ("rtg_group_reduce_ms", C.c_double, [C.c_void_p]),
@@ -118,7 +121,7 @@ RTG_EXPORTS = [
     # own-tile film exchange (rtg_multi.hip)
     ("rtg_tile_pixels", C.c_int, [C.c_uint32, C.c_uint32, u32p, C.c_uint32, u32p, u32p]),
     ("rtg_film_gather", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
-    ("rtg_film_scatter", C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("rtg_film_scatter", C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
 ]
 
 RTH_EXPORTS = [

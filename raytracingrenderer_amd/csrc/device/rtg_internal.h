@@ -151,6 +151,10 @@ struct TraceIO {
     unsigned cap_n;            // rays the capture holds (work index space of the launch)
     float4 cam_o;              // closest: the origin of every ray when ray_o is null (camera rays);
                                // a null queue is the identity (path id = ray index)
+    unsigned* hcnt;            // non-null (big waited-for chunks): block 0 stores the 8 extension
+                               // segment counts (seg_ne) here as the launch starts, with system-scope
+                               // stores to host-coherent memory, and the host sizes the next k_shade
+                               // grid from them (rtg_handle::h_cnt) without a device-to-host copy
 };
 
 struct ChunkArgs {
@@ -348,15 +352,17 @@ struct rtg_handle {
     rtg_stats stats{};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> kev;  // per-launch timing events (timing mode)
-    // k_shade's grid: the segment counts of every bounce's extension queue read back (pinned, one
-    // 1-KB Counters::ne8 block per bounce) while the next traversal runs, so the launch covers the
-    // live tiles only
+    // k_shade's grid (big waited-for chunks): the 8 segment counts of bounce b's extension queue,
+    // stored into host-coherent memory by k_trace(b)'s block 0 as it starts (TraceIO::hcnt; 8 per
+    // bounce, RTG_CNT_PENDING until written), so the host launches k_shade(b) while k_trace(b) runs.
+    // (Until round 5 a hipMemcpyAsync on a side stream read them back: its blit kernel queued behind
+    // the persistent k_trace for a CU slot, ~4.7 ms per copy, and the host launch waited for it.)
     unsigned* h_cnt = nullptr;
+    unsigned* d_hcnt = nullptr;   // the same memory, device address
     int cap_cnt = 0;
-    std::vector<hipEvent_t> cev;  // [b]: bounce b's counts are in h_cnt (on cstream)
-    std::vector<hipEvent_t> sev;  // [b]: k_shade producing them has finished (on the render stream)
-    hipStream_t cstream = nullptr;  // the read-backs, off the render stream
+    std::vector<hipEvent_t> tev;  // [b]: k_trace(b) has finished (a launch that never wrote its counts)
 };
+#define RTG_CNT_PENDING 0xFFFFFFFFu
 
 
 // The device records of a scene, built on the host from an rtg_scene_desc (prepare_scene) and

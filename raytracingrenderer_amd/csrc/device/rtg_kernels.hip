@@ -31,6 +31,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 // ------------------------------------------------------------------ traversal
@@ -87,6 +88,9 @@ void k_trace(SceneView s, TraceIO io) {
         s_tab[0][tid] = elo;
         s_tab[1][tid] = elen;
         s_tab[2][tid] = len;
+        // the host's next k_shade grid (TraceIO::hcnt): a volatile vector store, emitted with the
+        // system-scope bits (sc0 sc1). (__hip_atomic_store at system scope cost the walk 4 VGPR spills)
+        if (io.hcnt && blockIdx.x == 0) ((volatile unsigned*)io.hcnt)[tid] = elen;
     }
     if (SMALL)
         for (int i = tid; i < s.img_n4; i += RTG_TTB) s_img[i] = s.img[i];
@@ -1559,9 +1563,7 @@ void rtg_destroy(rtg_handle* h) {
     (void)hipFree(h->d_pix); (void)hipFree(h->d_qctr); (void)hipFree(h->d_stats);
     for (auto& e : h->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : h->kev) (void)hipEventDestroy(e);
-    for (auto& e : h->cev) (void)hipEventDestroy(e);
-    for (auto& e : h->sev) (void)hipEventDestroy(e);
-    if (h->cstream) (void)hipStreamDestroy(h->cstream);
+    for (auto& e : h->tev) (void)hipEventDestroy(e);
     if (h->h_cnt) (void)hipHostFree(h->h_cnt);
     (void)hipFree(h->d_cap); (void)hipFree(h->d_cap_len); (void)hipFree(h->d_cap_rays);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -1703,6 +1705,34 @@ const char* roctx_stage_name(int kind, int b) {
     return kind ? shade[b] : trace[b];
 }
 
+// The 8 segment counts of bounce b that k_trace(b)'s block 0 stores into h_cnt as it starts. The
+// host polls the host-coherent words; a launch that ended (or failed) without writing them is an
+// error, not a hang.
+static int wait_counts(rtg_handle* h, int b) {
+    unsigned* c = h->h_cnt + 8 * b;
+    auto ready = [&]() {
+        for (int k = 0; k < 8; ++k)
+            if (__atomic_load_n(c + k, __ATOMIC_ACQUIRE) == RTG_CNT_PENDING) return false;
+        return true;
+    };
+    for (unsigned spin = 1;; ++spin) {
+        if (ready()) return RTG_OK;
+        if ((spin & 255u) == 0) {
+            const hipError_t e = hipEventQuery(h->tev[b]);
+            if (e == hipSuccess) {
+                if (ready()) return RTG_OK;
+                g_err = "k_trace finished without storing its segment counts";
+                return RTG_ERR_HIP;
+            }
+            if (e != hipErrorNotReady) {
+                g_err = std::string("k_trace (segment counts): ") + hipGetErrorString(e);
+                return RTG_ERR_HIP;
+            }
+            std::this_thread::yield();
+        }
+    }
+}
+
 int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed,
                        const uint32_t* tiles, uint32_t n_tiles, hipStream_t st, bool lazy, bool add_spp) {
     RoctxRange r_render(lazy ? "rtg:render (queued chunks)" : "rtg:render");
@@ -1769,17 +1799,17 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                                              std::max(h->trace_blocks_small, h->trace_blocks_small_count)) * (RTG_TTB / 64);
     if (h->cap_cnt < maxb + 1) {
         if (h->h_cnt) (void)hipHostFree(h->h_cnt);
-        h->h_cnt = nullptr;
+        h->h_cnt = h->d_hcnt = nullptr;
         h->cap_cnt = 0;
-        HIPOK(hipHostMalloc((void**)&h->h_cnt, (size_t)(maxb + 1) * 256 * sizeof(unsigned), hipHostMallocDefault));
+        HIPOK(hipHostMalloc((void**)&h->h_cnt, (size_t)(maxb + 1) * 8 * sizeof(unsigned),
+                            hipHostMallocCoherent | hipHostMallocMapped));
+        HIPOK(hipHostGetDevicePointer((void**)&h->d_hcnt, h->h_cnt, 0));
         h->cap_cnt = maxb + 1;
     }
-    while ((int)h->cev.size() < maxb + 1) {
-        hipEvent_t e, f;
+    while ((int)h->tev.size() < maxb + 1) {
+        hipEvent_t e;
         HIPOK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        h->cev.push_back(e);
-        HIPOK(hipEventCreateWithFlags(&f, hipEventDisableTiming));
-        h->sev.push_back(f);
+        h->tev.push_back(e);
     }
     uint32_t c = 0;
     for (uint32_t s0 = first; s0 < first + n_samples; s0 += ns_chunk, ++c) {
@@ -1817,7 +1847,6 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         // k_shade grids from the live counts read back while the traversal runs (big chunks), or over
         // every tile a segment can hold (blocks past the live count exit at once): no host wait
         const bool hostgrid = !pipe && (a.seg_tiles >= RTG_HOSTGRID_MIN_TILES || h->serial);
-        if (hostgrid && !h->cstream) HIPOK(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
         HIPOK(hipMemsetAsync(pb.ctr, 0, (size_t)(maxb + 1) * sizeof(Counters), ss));
         timed_begin(h, ss, k);
         {
@@ -1840,8 +1869,8 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                     if (b == 1) {
                         live = a.P > sgm * cap ? std::min(cap, a.P - sgm * cap) : 0u;
                     } else {
-                        if (sgm == 0) HIPOK(hipEventSynchronize(h->cev[b - 1]));
-                        live = h->h_cnt[256 * (b - 1) + 32 * sgm];
+                        if (sgm == 0 && (rc = wait_counts(h, b - 1))) return rc;
+                        live = h->h_cnt[8 * (b - 1) + sgm];
                     }
                     tiles = std::max(tiles, (live + RTG_TB - 1) / RTG_TB);
                 }
@@ -1851,13 +1880,6 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                     const bool alt = h->integrator != RTG_INTEGRATOR_PATH;
                     if (int rc_ = launch_shade(alt, tab, 8 * tiles, ss, h->sv, a, pb, b - 1)) return rc_;
                     timed_end(h, ss, k); kinds.push_back(2); ++k;
-                }
-                if (hostgrid && b < maxb) {  // the next bounce's segment counts, for its k_shade grid
-                    HIPOK(hipEventRecord(h->sev[b], ss));
-                    HIPOK(hipStreamWaitEvent(h->cstream, h->sev[b], 0));
-                    HIPOK(hipMemcpyAsync(h->h_cnt + 256 * b, pb.ctr[b].ne8, 256 * sizeof(unsigned),
-                                         hipMemcpyDeviceToHost, h->cstream));
-                    HIPOK(hipEventRecord(h->cev[b], h->cstream));
                 }
             }
             // extension payload by queue position (set b & 1; null queue: path id = position);
@@ -1886,6 +1908,12 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             io.wtime = (d_wt && c == 0) ? d_wt + (size_t)b * wt_waves * 3 : nullptr;
             io.cap = nullptr;
             io.cap_len = nullptr;
+            // k_trace(b) hands the host bounce b's segment counts, for k_shade(b)'s grid
+            io.hcnt = nullptr;
+            if (hostgrid && b > 0 && b < maxb) {
+                for (int k = 0; k < 8; ++k) __atomic_store_n(h->h_cnt + 8 * b + k, RTG_CNT_PENDING, __ATOMIC_RELAXED);
+                io.hcnt = h->d_hcnt + 8 * b;
+            }
             if (RTG_DEBUG && c == 0 && b == h->capture_launch) {
                 const size_t cn = 2 * (size_t)a.seg_tiles * 8 * RTG_TB;  // both index spans
                 (void)hipFree(h->d_cap);
@@ -1909,6 +1937,7 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
                 if ((rc = launch_trace(h, io, ss))) return rc;
             }
             timed_end(h, ss, k); kinds.push_back(0); ++k;
+            if (io.hcnt) HIPOK(hipEventRecord(h->tev[b], ss));
         }
         hipLaunchKernelGGL(k_tally, dim3(1), dim3(64), 0, ss, pb.ctr, maxb, h->d_stats);
         LAUNCH_OK("k_tally");

@@ -78,27 +78,21 @@ bool load_rccl() {
     return g_rccl.ok;
 }
 
-// the reduce's two timing events on device 0, destroyed on every return path
-struct EventPair {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    ~EventPair() {
-        if (e0) (void)hipEventDestroy(e0);
-        if (e1) (void)hipEventDestroy(e1);
-    }
-};
 }  // namespace
 
 // Own-tile film exchange. Pack: dst[i] = film[pix[i]] (3 floats; a padding index packs zeros).
 // Scatter: film[pix[i]] = src[i] (padding skipped). One thread per pixel, 12-B reads and writes:
 // HBM-bound, 24 B per pixel moved.
 #define RTG_PIX_PAD 0xFFFFFFFFu
+// An index at or past the film's pixel count (a list built for another film size) is treated as
+// padding: packed as zeros, skipped by the scatter, never dereferenced.
 __global__ __launch_bounds__(256) void k_film_gather(const float* __restrict__ film, const uint32_t* __restrict__ pix,
-                                                     uint32_t n, float* __restrict__ dst) {
+                                                     uint32_t n, uint32_t film_pixels, float* __restrict__ dst) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     const uint32_t p = pix[i];
     float r = 0.0f, g = 0.0f, b = 0.0f;
-    if (p != RTG_PIX_PAD) {
+    if (p < film_pixels) {
         r = film[3 * (size_t)p];
         g = film[3 * (size_t)p + 1];
         b = film[3 * (size_t)p + 2];
@@ -109,11 +103,11 @@ __global__ __launch_bounds__(256) void k_film_gather(const float* __restrict__ f
 }
 
 __global__ __launch_bounds__(256) void k_film_scatter(const float* __restrict__ src, const uint32_t* __restrict__ pix,
-                                                      uint32_t n, float* __restrict__ film) {
+                                                      uint32_t n, uint32_t film_pixels, float* __restrict__ film) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n) return;
     const uint32_t p = pix[i];
-    if (p == RTG_PIX_PAD) return;
+    if (p >= film_pixels) return;  // padding (RTG_PIX_PAD) or out of range
     film[3 * (size_t)p] = src[3 * (size_t)i];
     film[3 * (size_t)p + 1] = src[3 * (size_t)i + 1];
     film[3 * (size_t)p + 2] = src[3 * (size_t)i + 2];
@@ -150,6 +144,14 @@ struct rtg_group {
     bool poisoned = false;                     // a rank failed a render: films hold partial samples
     double reduce_ms = 0.0;
     double prepare_ms = 0.0, upload_ms = 0.0;  // group setup: host build once, parallel uploads
+    // the exchange's own streams, one per rank on its device (rank r: its pack and send; devices[0]
+    // also the receives and the scatter), so that a queued exchange (rtg_group_reduce_async) runs
+    // beside the ranks' next frames instead of in their render streams
+    std::vector<hipStream_t> xs;
+    std::vector<hipEvent_t> xpacked;           // repeated devices: rank r's pack is done
+    hipEvent_t xcopied = nullptr;              // repeated devices: devices[0] has copied every pack
+    hipEvent_t xe0 = nullptr, xe1 = nullptr;   // devices[0]: rank 0's frames on its film / scatter done
+    bool xtimed = false;                       // xe0 / xe1 hold an exchange not yet read into reduce_ms
 };
 
 // the own-tile exchange's buffers: per rank its pixel list + pack buffer on its device, on devices[0]
@@ -168,13 +170,65 @@ static int exchange_setup(rtg_group* g) {
     HIPOK(hipSetDevice(g->devices[0]));
     HIPOK(hipMalloc((void**)&g->d_recv, n * mp * 3 * sizeof(float)));
     if (dev_upload(&g->d_pix_all, all)) return RTG_ERR_HIP;
+    HIPOK(hipEventCreate(&g->xe0));
+    HIPOK(hipEventCreate(&g->xe1));
+    HIPOK(hipEventCreateWithFlags(&g->xcopied, hipEventDisableTiming));
     g->d_pix.assign(n, nullptr);
     g->d_pack.assign(n, nullptr);
+    g->xs.assign(n, nullptr);
+    g->xpacked.assign(n, nullptr);
     for (size_t r = 0; r < n; ++r) {
         HIPOK(hipSetDevice(g->devices[r]));
         if (dev_upload(&g->d_pix[r], pl[r])) return RTG_ERR_HIP;
         if (r == 0) g->d_pack[r] = g->d_recv;
         else HIPOK(hipMalloc((void**)&g->d_pack[r], mp * 3 * sizeof(float)));
+        HIPOK(hipStreamCreateWithFlags(&g->xs[r], hipStreamNonBlocking));
+        HIPOK(hipEventCreateWithFlags(&g->xpacked[r], hipEventDisableTiming));
+    }
+    return RTG_OK;
+}
+
+// Runs fn(r) for every rank: one host thread per rank when every rank has a device of its own (a
+// rank's call may wait on the host: back-pressure of the frame pipeline, a big chunk's count
+// read-backs), in turn otherwise. The first failing rank's code is returned and the group poisoned.
+template <class F>
+static int for_ranks(rtg_group* g, F fn) {
+    const size_t n = g->h.size();
+    std::vector<int> rc(n, RTG_OK);
+    std::vector<std::string> err(n);
+    auto run = [&](size_t r) {
+        rc[r] = fn(r);
+        if (rc[r]) err[r] = rtg_last_error();  // g_err is thread-local
+    };
+    if (n == 1 || !g->distinct) {
+        for (size_t r = 0; r < n; ++r) run(r);
+    } else {
+        std::vector<std::thread> pool;
+        for (size_t r = 0; r < n; ++r) pool.emplace_back(run, r);
+        for (auto& t : pool) t.join();
+    }
+    for (size_t r = 0; r < n; ++r)
+        if (rc[r]) {
+            g->poisoned = true;
+            g_err = "rank " + std::to_string(r) + ": " + err[r] + " (group films now partial: rtg_group_clear)";
+            return rc[r];
+        }
+    return RTG_OK;
+}
+
+// every rank's queued frames and the queued exchanges have finished; the last exchange's device time
+// goes to reduce_ms
+static int group_sync(rtg_group* g) {
+    for (size_t r = 0; r < g->h.size(); ++r) {
+        if (int rc = rtg_synchronize(g->h[r])) return rc;
+        HIPOK(hipSetDevice(g->devices[r]));
+        if (r < g->xs.size() && g->xs[r]) HIPOK(hipStreamSynchronize(g->xs[r]));
+    }
+    if (g->xtimed) {
+        float ms = 0.0f;
+        HIPOK(hipSetDevice(g->devices[0]));
+        if (hipEventElapsedTime(&ms, g->xe0, g->xe1) == hipSuccess) g->reduce_ms = ms;
+        g->xtimed = false;
     }
     return RTG_OK;
 }
@@ -214,7 +268,7 @@ int rtg_film_gather(rtg_handle* h, const uint32_t* pixels_dev, uint32_t n, float
     }
     if (n) {
         hipLaunchKernelGGL(k_film_gather, dim3((n + 255) / 256), dim3(256), 0, st, (const float*)h->d_film, pixels_dev, n,
-                           dst_dev);
+                           (uint32_t)h->W * (uint32_t)h->H, dst_dev);
         LAUNCH_OK("k_film_gather");
         if (st != h->stream) {
             // the handle's later film writes (the next renders' folds wait on its stream) come after
@@ -227,15 +281,15 @@ int rtg_film_gather(rtg_handle* h, const uint32_t* pixels_dev, uint32_t n, float
 }
 
 int rtg_film_scatter(int device, const float* src_dev, const uint32_t* pixels_dev, uint32_t n, float* film_dev,
-                     void* stream) {
-    if (n && (!src_dev || !pixels_dev || !film_dev)) {
+                     uint32_t film_pixels, void* stream) {
+    if (n && (!src_dev || !pixels_dev || !film_dev || !film_pixels)) {
         g_err = "rtg_film_scatter: bad argument";
         return RTG_ERR_ARG;
     }
     HIPOK(hipSetDevice(device));
     if (n) {
         hipLaunchKernelGGL(k_film_scatter, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, src_dev, pixels_dev,
-                           n, film_dev);
+                           n, film_pixels, film_dev);
         LAUNCH_OK("k_film_scatter");
     }
     return RTG_OK;
@@ -259,17 +313,23 @@ int rtg_tiles_for_rank(uint32_t width, uint32_t height, int rank, int world, uin
 
 void rtg_group_destroy(rtg_group* g) {
     if (!g) return;
+    (void)group_sync(g);  // queued frames and exchanges still use the buffers
     for (ncclComm_t c : g->comms) (void)g_rccl.comm_destroy(c);
     for (size_t r = 0; r < g->d_pix.size(); ++r) {
         (void)hipSetDevice(g->devices[r]);
         (void)hipFree(g->d_pix[r]);
         if (r > 0) (void)hipFree(g->d_pack[r]);  // rank 0 packs straight into d_recv
+        if (r < g->xs.size() && g->xs[r]) (void)hipStreamDestroy(g->xs[r]);
+        if (r < g->xpacked.size() && g->xpacked[r]) (void)hipEventDestroy(g->xpacked[r]);
     }
     if (!g->devices.empty()) {
         (void)hipSetDevice(g->devices[0]);
         (void)hipFree(g->d_sum);
         (void)hipFree(g->d_recv);
         (void)hipFree(g->d_pix_all);
+        if (g->xe0) (void)hipEventDestroy(g->xe0);
+        if (g->xe1) (void)hipEventDestroy(g->xe1);
+        if (g->xcopied) (void)hipEventDestroy(g->xcopied);
     }
     for (rtg_handle* h : g->h) rtg_destroy(h);
     delete g;
@@ -391,33 +451,34 @@ int rtg_group_set_options(rtg_group* g, int max_depth, int flags, uint32_t max_p
 
 int rtg_group_render(rtg_group* g, uint32_t first_sample, uint32_t n_samples, uint64_t seed) {
     if (!g) return RTG_ERR_ARG;
-    const size_t n = g->h.size();
-    std::vector<int> rc(n, RTG_OK);
-    std::vector<std::string> err(n);
-    auto run = [&](size_t r) {
-        const std::vector<uint32_t>& t = g->tiles[r];
-        if (t.empty()) return;  // more devices than tiles: this rank's film stays zero
-        rc[r] = rtg_render(g->h[r], first_sample, n_samples, seed, t.data(), (uint32_t)t.size());
-        if (rc[r]) err[r] = rtg_last_error();  // g_err is thread-local
-    };
-    if (n == 1 || !g->distinct) {
-        for (size_t r = 0; r < n; ++r) run(r);  // one device: ranks in turn
-    } else {
-        std::vector<std::thread> pool;
-        for (size_t r = 0; r < n; ++r) pool.emplace_back(run, r);
-        for (auto& t : pool) t.join();
-    }
     g->reduced = false;
-    for (size_t r = 0; r < n; ++r)
-        if (rc[r]) {
-            g->poisoned = true;
-            g_err = "rank " + std::to_string(r) + ": " + err[r] + " (group films now partial: rtg_group_clear)";
-            return rc[r];
-        }
-    return RTG_OK;
+    return for_ranks(g, [&](size_t r) {
+        const std::vector<uint32_t>& t = g->tiles[r];
+        if (t.empty()) return (int)RTG_OK;  // more devices than tiles: this rank's film stays zero
+        return rtg_render(g->h[r], first_sample, n_samples, seed, t.data(), (uint32_t)t.size());
+    });
 }
 
-int rtg_group_reduce(rtg_group* g) {
+// The queued frame of a group (the frame loop of Main.cpp:74-118 on N devices): every rank's
+// rtg_render_async on its own device, so the ranks' frames are coalesced and pipelined exactly as one
+// handle's are, and the call returns without waiting for the GPUs (a rank's call waits only for the
+// frame pipeline's back-pressure or a big chunk's count read-backs, on its own host thread).
+int rtg_group_render_async(rtg_group* g, uint32_t first_sample, uint32_t n_samples, uint64_t seed) {
+    if (!g) return RTG_ERR_ARG;
+    g->reduced = false;
+    return for_ranks(g, [&](size_t r) {
+        const std::vector<uint32_t>& t = g->tiles[r];
+        if (t.empty()) return (int)RTG_OK;
+        return rtg_render_async(g->h[r], first_sample, n_samples, seed, t.data(), (uint32_t)t.size(), nullptr);
+    });
+}
+
+// The own-tile exchange, queued on the exchange streams (xs): rank r packs its tiles' pixels once
+// its queued frames are on its film (rtg_film_gather: the handle's later folds wait for the pack, so
+// the next frames' traversals run on meanwhile), sends them to devices[0] (one ncclSend / ncclRecv
+// pair per rank inside one RCCL group), and devices[0] scatters every rank's pixels into the
+// assembled film. No host wait.
+int rtg_group_reduce_async(rtg_group* g) {
     if (!g) return RTG_ERR_ARG;
     if (g->poisoned) {
         g_err = "rtg_group_reduce: a rank failed its last render; the films are partial until rtg_group_clear";
@@ -425,14 +486,15 @@ int rtg_group_reduce(rtg_group* g) {
     }
     const size_t n = g->h.size();
     const size_t mp = std::max<uint32_t>(g->maxpix, 1);
-    EventPair ev;
+    const uint32_t film_pixels = g->W * g->H;
+    // timing: from rank 0's frames being on its film (a gather of no pixels is only that wait) to
+    // the scatter's end; the other ranks' frames and the transfers are inside the pair
+    if (int rc = rtg_film_gather(g->h[0], nullptr, 0, nullptr, g->xs[0])) return rc;
     HIPOK(hipSetDevice(g->devices[0]));
-    HIPOK(hipEventCreate(&ev.e0));
-    HIPOK(hipEventCreate(&ev.e1));
-    HIPOK(hipEventRecord(ev.e0, g->h[0]->stream));
+    HIPOK(hipEventRecord(g->xe0, g->xs[0]));
     // every rank packs its own tiles' pixels on its device (rank 0 straight into the receive buffer)
     for (size_t r = 0; r < n; ++r)
-        if (int rc = rtg_film_gather(g->h[r], g->d_pix[r], g->npix[r], g->d_pack[r], nullptr)) return rc;
+        if (int rc = rtg_film_gather(g->h[r], g->d_pix[r], g->npix[r], g->d_pack[r], g->xs[r])) return rc;
     if (!g->comms.empty()) {
         // one ncclSend per rank > 0 to device 0, which posts the matching ncclRecv into slot r of its
         // receive buffer. Every failure inside the group still closes it (ncclGroupEnd), so the
@@ -442,42 +504,52 @@ int rtg_group_reduce(rtg_group* g) {
         for (size_t r = 1; r < n && fail.empty(); ++r) {
             if (!g->npix[r]) continue;
             const size_t cnt = (size_t)g->npix[r] * 3;
-            ncclResult_t nr = g_rccl.send(g->d_pack[r], cnt, ncclFloat, 0, g->comms[r], g->h[r]->stream);
+            ncclResult_t nr = g_rccl.send(g->d_pack[r], cnt, ncclFloat, 0, g->comms[r], g->xs[r]);
             if (nr == ncclSuccess)
-                nr = g_rccl.recv(g->d_recv + r * mp * 3, cnt, ncclFloat, (int)r, g->comms[0], g->h[0]->stream);
+                nr = g_rccl.recv(g->d_recv + r * mp * 3, cnt, ncclFloat, (int)r, g->comms[0], g->xs[0]);
             if (nr != ncclSuccess) fail = std::string("ncclSend/ncclRecv: ") + g_rccl.error_string(nr);
         }
         const ncclResult_t nr = g_rccl.group_end();
         if (!fail.empty()) { g_err = fail; return RTG_ERR_HIP; }
         if (nr != ncclSuccess) { g_err = std::string("ncclGroupEnd: ") + g_rccl.error_string(nr); return RTG_ERR_HIP; }
-    } else {
-        // repeated devices: the packed tiles move with device copies, in rank order
+    } else if (n > 1) {
+        // repeated devices: the packs move with device copies on devices[0]'s exchange stream, each
+        // after its pack; the next packs wait for the copies
         for (size_t r = 1; r < n; ++r) {
             if (!g->npix[r]) continue;
             HIPOK(hipSetDevice(g->devices[r]));
-            HIPOK(hipStreamSynchronize(g->h[r]->stream));
+            HIPOK(hipEventRecord(g->xpacked[r], g->xs[r]));
             HIPOK(hipSetDevice(g->devices[0]));
+            HIPOK(hipStreamWaitEvent(g->xs[0], g->xpacked[r], 0));
             HIPOK(hipMemcpyPeerAsync(g->d_recv + r * mp * 3, g->devices[0], g->d_pack[r], g->devices[r],
-                                     (size_t)g->npix[r] * 3 * sizeof(float), g->h[0]->stream));
+                                     (size_t)g->npix[r] * 3 * sizeof(float), g->xs[0]));
+        }
+        HIPOK(hipSetDevice(g->devices[0]));
+        HIPOK(hipEventRecord(g->xcopied, g->xs[0]));
+        for (size_t r = 1; r < n; ++r) {
+            HIPOK(hipSetDevice(g->devices[r]));
+            HIPOK(hipStreamWaitEvent(g->xs[r], g->xcopied, 0));
         }
     }
-    HIPOK(hipSetDevice(g->devices[0]));
-    HIPOK(hipMemsetAsync(g->d_sum, 0, (size_t)g->W * g->H * 3 * sizeof(float), g->h[0]->stream));
-    if (int rc = rtg_film_scatter(g->devices[0], g->d_recv, g->d_pix_all, (uint32_t)(n * mp), g->d_sum, g->h[0]->stream))
+    // tile supports cover the film, so the scatter writes every pixel of d_sum
+    if (int rc = rtg_film_scatter(g->devices[0], g->d_recv, g->d_pix_all, (uint32_t)(n * mp), g->d_sum, film_pixels,
+                                  g->xs[0]))
         return rc;
-    HIPOK(hipEventRecord(ev.e1, g->h[0]->stream));
-    for (size_t r = 1; r < n && !g->comms.empty(); ++r) {
-        HIPOK(hipSetDevice(g->devices[r]));
-        HIPOK(hipStreamSynchronize(g->h[r]->stream));
-    }
-    HIPOK(hipSetDevice(g->devices[0]));
-    HIPOK(hipEventSynchronize(ev.e1));
-    float ms = 0.0f;
-    (void)hipEventElapsedTime(&ms, ev.e0, ev.e1);
-    g->reduce_ms = ms;
+    HIPOK(hipEventRecord(g->xe1, g->xs[0]));
+    g->xtimed = true;
     g->reduced_spp = g->h[0]->spp;
     g->reduced = true;
     return RTG_OK;
+}
+
+int rtg_group_reduce(rtg_group* g) {
+    if (int rc = rtg_group_reduce_async(g)) return rc;
+    return group_sync(g);
+}
+
+int rtg_group_synchronize(rtg_group* g) {
+    if (!g) return RTG_ERR_ARG;
+    return group_sync(g);
 }
 
 int rtg_group_film_read(rtg_group* g, float* rgb_sum, uint32_t* spp) {
@@ -487,6 +559,7 @@ int rtg_group_film_read(rtg_group* g, float* rgb_sum, uint32_t* spp) {
         if (rc) return rc;
     }
     HIPOK(hipSetDevice(g->devices[0]));
+    HIPOK(hipStreamSynchronize(g->xs[0]));  // a queued exchange (the copy below does not order with it)
     if (rgb_sum) HIPOK(hipMemcpy(rgb_sum, g->d_sum, (size_t)g->W * g->H * 3 * sizeof(float), hipMemcpyDeviceToHost));
     if (spp) *spp = g->reduced_spp;
     return RTG_OK;
@@ -494,6 +567,7 @@ int rtg_group_film_read(rtg_group* g, float* rgb_sum, uint32_t* spp) {
 
 int rtg_group_clear(rtg_group* g) {
     if (!g) return RTG_ERR_ARG;
+    if (int rc = group_sync(g)) return rc;
     for (rtg_handle* h : g->h) {
         const int rc = rtg_clear(h);
         if (rc) return rc;

@@ -15,10 +15,11 @@
 // queued frames a call returns once the frame three before it has left the GPU, so in the steady
 // state it is the GPU's time per frame.
 // Multi-GPU (one node): -gpus N renders on devices 0..N-1, -devices a,b,... on a list. Rank r
-// renders the 32x32 tiles with (tile_x + tile_y) % N == r, one host thread per device, and the film is
-// assembled on the first device from every device's own tiles (packed, one RCCL send per device,
-// scattered) before it is written (rtg_group_*, include/rtg.h); the output is bit-identical to the
-// one-device render.
+// renders the 32x32 tiles with (tile_x + tile_y) % N == r, and the film is assembled on the first
+// device from every device's own tiles (packed, one RCCL send per device, scattered) before it is
+// written (rtg_group_*, include/rtg.h); the output is bit-identical to the one-device render. Frames
+// are queued on every device (rtg_group_render_async: coalesced and pipelined per device, as on one
+// device) unless -sync 1 (rtg_group_render: each call waits for every device).
 #include "../../../include/rth.h"
 
 #include <chrono>
@@ -98,7 +99,7 @@ int main(int argc, char** argv) {
     while (spp < spp_target) {
         const unsigned n = std::min(batch, spp_target - spp);
         auto t0 = std::chrono::steady_clock::now();
-        const int rc = grp    ? rtg_group_render(grp, spp, n, seed)
+        const int rc = grp    ? (sync ? rtg_group_render(grp, spp, n, seed) : rtg_group_render_async(grp, spp, n, seed))
                        : sync ? rtg_render(rt, spp, n, seed, nullptr, 0)
                               : rtg_render_async(rt, spp, n, seed, nullptr, 0, nullptr);
         if (rc != 0) return die("rtg_render", rtg_last_error());
@@ -111,9 +112,11 @@ int main(int argc, char** argv) {
     std::vector<float> film((size_t)info.width * info.height * 3);
     uint32_t got = 0;
     if (rt && rtg_synchronize(rt) != 0) return die("rtg_synchronize", rtg_last_error());
+    if (grp && rtg_group_synchronize(grp) != 0) return die("rtg_group_synchronize", rtg_last_error());
     const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
     std::printf("%u spp in %.4f s of wall time (%s): %.4f ms per spp, %.1f Mpaths/s\n", spp, wall,
-                grp ? "device group" : sync ? "synchronous calls" : "queued calls", 1e3 * wall / std::max(1u, spp),
+                grp ? (sync ? "device group, synchronous calls" : "device group, queued calls")
+                    : sync ? "synchronous calls" : "queued calls", 1e3 * wall / std::max(1u, spp),
                 (double)spp * info.width * info.height / wall / 1e6);
     if (grp) {
         if (rtg_group_film_read(grp, film.data(), &got) != 0) return die("rtg_group_film_read", rtg_last_error());

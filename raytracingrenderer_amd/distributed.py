@@ -120,7 +120,7 @@ class FilmExchange:
                 stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
                 rc = N.rtg().rtg_film_scatter(film_tensor.device.index, C.c_void_p(self.recv.data_ptr()),
                                               C.c_void_p(self.t_all.data_ptr()), len(self.all),
-                                              C.c_void_p(film_tensor.data_ptr()), stream)
+                                              C.c_void_p(film_tensor.data_ptr()), self.W * self.H, stream)
                 if rc:
                     raise RuntimeError(N.rtg().rtg_last_error().decode())
             else:
@@ -141,7 +141,9 @@ def render_sharded(rt, n_samples, rank, world, dist=None, film_tensor=None, firs
 
     world > 1: rank 0's film_tensor (torch float32 HxWx3) receives the whole film from every rank's
     own tiles (FilmExchange; pass `exchange` to reuse its buffers across calls); a CUDA tensor is
-    filled on the device (RCCL), a CPU tensor through host memory (gloo). Returns film_tensor.
+    filled on the device (RCCL), a CPU tensor through host memory (gloo). On the other ranks
+    film_tensor receives this rank's own film (its tiles' samples, zero elsewhere), as the
+    whole-film reduce of rounds 1-4 left it. Returns film_tensor.
     world == 1: returns film_tensor filled with the film if given, else the film as a numpy array."""
     tiles = tiles_for_rank(rt.width, rt.height, rank, world)
     rt.render(n_samples, tiles=tiles, first_sample=first_sample)
@@ -149,15 +151,23 @@ def render_sharded(rt, n_samples, rank, world, dist=None, film_tensor=None, firs
         if world > 1:
             raise ValueError("render_sharded: world > 1 needs a film_tensor to assemble into")
         return rt.film()[0]
-    if world == 1:
+
+    def own_film():
         if film_tensor.is_cuda:
             rt.copy_film_to(film_tensor.data_ptr())
             rt.synchronize()
         else:
             import torch
             film_tensor.copy_(torch.from_numpy(rt.film()[0]))
+    if world == 1:
+        own_film()
         return film_tensor
     if exchange is None:
         exchange = FilmExchange(rt.width, rt.height, rank, world, film_tensor.device if film_tensor.is_cuda else None)
+    if (exchange.W, exchange.H, exchange.rank, exchange.world) != (rt.width, rt.height, rank, world):
+        raise ValueError("render_sharded: exchange built for %dx%d rank %d of %d, not %dx%d rank %d of %d"
+                         % (exchange.W, exchange.H, exchange.rank, exchange.world, rt.width, rt.height, rank, world))
     exchange.exchange(rt, film_tensor, dist)
+    if rank != 0:
+        own_film()
     return film_tensor

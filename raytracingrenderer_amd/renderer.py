@@ -361,10 +361,16 @@ class RayTracerGroup:
         _check(self._lib.rtg_group_setup_ms(self._g, C.byref(a), C.byref(b)), self._lib.rtg_last_error)
         return a.value, b.value
 
-    def reduce(self):
+    def reduce(self, sync=True):
         """Assemble the film on devices[0] from every rank's own tiles (RCCL send/recv; device copies
-        for repeated devices); synchronous."""
-        _check(self._lib.rtg_group_reduce(self._g), self._lib.rtg_last_error)
+        for repeated devices). sync=False queues it on the exchange streams after every rank's queued
+        frames (rtg_group_reduce_async): the ranks' next frames run on meanwhile."""
+        fn = self._lib.rtg_group_reduce if sync else self._lib.rtg_group_reduce_async
+        _check(fn(self._g), self._lib.rtg_last_error)
+
+    def synchronize(self):
+        """Wait for every rank's queued frames and the queued exchanges (rtg_group_synchronize)."""
+        _check(self._lib.rtg_group_synchronize(self._g), self._lib.rtg_last_error)
 
     def rank_stats(self):
         """rtg_get_stats of every rank's handle (rays, kernel ms, counting-pass counters)."""
@@ -385,9 +391,12 @@ class RayTracerGroup:
     def uses_rccl(self):
         return bool(self._lib.rtg_group_uses_rccl(self._g))
 
-    def render(self, n_samples=1, first_sample=None):
+    def render(self, n_samples=1, first_sample=None, sync=True):
+        """Every rank adds n_samples samples of its tiles. sync=False queues the frame on every rank
+        (rtg_group_render_async: coalesced and pipelined per rank, as RayTracer.render(sync=False))."""
         first = self._spp if first_sample is None else first_sample
-        _check(self._lib.rtg_group_render(self._g, first, n_samples, self.seed), self._lib.rtg_last_error)
+        fn = self._lib.rtg_group_render if sync else self._lib.rtg_group_render_async
+        _check(fn(self._g, first, n_samples, self.seed), self._lib.rtg_last_error)
         self._spp = first + n_samples
 
     def film(self):

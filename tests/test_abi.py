@@ -31,7 +31,7 @@ def test_exports_cover_header(header, lib):
 
 
 def test_abi_version():
-    assert N.rtg().rtg_abi_version() == 5
+    assert N.rtg().rtg_abi_version() == 6
 
 
 def test_build_ids_match_the_tree():

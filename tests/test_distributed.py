@@ -121,8 +121,7 @@ def _gpu_worker(rank, world, port, out_path):
     rt = RayTracer(s, seed=77)
     t = torch.zeros((80, 96, 3), dtype=torch.float32)
     render_sharded(rt, 3, rank, world, dist=dist, film_tensor=t)
-    if rank == 0:
-        np.save(out_path, t.numpy())
+    np.save(out_path if rank == 0 else out_path + ".rank%d.npy" % rank, t.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -130,8 +129,10 @@ def _gpu_worker(rank, world, port, out_path):
 @pytest.mark.gpu
 def test_librtg_ranks_reduce_is_bit_exact(tmp_path):
     """Two processes, each with its own librtg handle, reduce their tile films over gloo: the
-    result equals one handle rendering every tile, bit for bit."""
+    result equals one handle rendering every tile, bit for bit; rank 1's film_tensor holds its own
+    tiles' film (render_sharded fills it on the non-root ranks)."""
     import torch.multiprocessing as mp
+    from raytracingrenderer_amd.distributed import tiles_for_rank
     out = str(tmp_path / "film.npy")
     mp.spawn(_gpu_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     from raytracingrenderer_amd import RayTracer, loadScene
@@ -141,6 +142,9 @@ def test_librtg_ranks_reduce_is_bit_exact(tmp_path):
     full = rt.film()[0]
     got = np.load(out)
     assert np.array_equal(got.view(np.uint32), full.view(np.uint32))
+    own = RayTracer(s, seed=77)
+    own.render(3, tiles=tiles_for_rank(96, 80, 1, 2), first_sample=0)
+    assert np.array_equal(np.load(out + ".rank1.npy").view(np.uint32), own.film()[0].view(np.uint32))
 
 
 @pytest.mark.gpu
@@ -196,9 +200,45 @@ def test_device_gather_scatter_assemble_one_render(world):
         del rt
     film = torch.full((H, W, 3), float("nan"), dtype=torch.float32, device="cuda:0")
     assert N.rtg().rtg_film_scatter(0, C.c_void_p(recv.data_ptr()), C.c_void_p(fx[0].t_all.data_ptr()),
-                                    len(fx[0].all), C.c_void_p(film.data_ptr()), None) == 0
+                                    len(fx[0].all), C.c_void_p(film.data_ptr()), W * H, None) == 0
     torch.cuda.synchronize()
     assert np.array_equal(film.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gather_scatter_ignore_indices_past_the_film():
+    """A pixel list built for a larger film (or any index >= width * height) is never dereferenced:
+    rtg_film_gather packs zeros for it and rtg_film_scatter skips it; in-range entries move as usual."""
+    import ctypes as C
+    import torch
+    from raytracingrenderer_amd import RayTracer, loadScene
+    from raytracingrenderer_amd import _native as N
+    W, H = 64, 48
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=W, height=H)
+    rt = RayTracer(s, seed=5)
+    rt.render(2, first_sample=0)
+    want = rt.film()[0].reshape(-1, 3)
+    pix = np.array([3, W * H, W * H - 1, 0xFFFFFFFE, 7 * W + 5, 1 << 30], np.uint32)
+    t_pix = torch.from_numpy(pix.view(np.int32)).to("cuda:0")
+    pack = torch.full((len(pix) * 3,), float("nan"), dtype=torch.float32, device="cuda:0")
+    assert N.rtg().rtg_film_gather(rt.handle, C.c_void_p(t_pix.data_ptr()), len(pix), C.c_void_p(pack.data_ptr()),
+                                   None) == 0
+    rt.synchronize()
+    got = pack.cpu().numpy().reshape(-1, 3)
+    ok = pix < W * H
+    assert np.array_equal(got[ok].view(np.uint32), want[pix[ok]].view(np.uint32))
+    assert not got[~ok].view(np.uint32).any()
+    film = torch.full((H * W * 3,), float("nan"), dtype=torch.float32, device="cuda:0")
+    assert N.rtg().rtg_film_scatter(0, C.c_void_p(pack.data_ptr()), C.c_void_p(t_pix.data_ptr()), len(pix),
+                                    C.c_void_p(film.data_ptr()), W * H, None) == 0
+    torch.cuda.synchronize()
+    f = film.cpu().numpy().reshape(-1, 3)
+    assert np.array_equal(f[pix[ok]].view(np.uint32), want[pix[ok]].view(np.uint32))
+    written = np.zeros(W * H, bool)
+    written[pix[ok]] = True
+    assert np.isnan(f[~written]).all()
+    assert N.rtg().rtg_film_scatter(0, C.c_void_p(pack.data_ptr()), C.c_void_p(t_pix.data_ptr()), len(pix),
+                                    C.c_void_p(film.data_ptr()), 0, None) != 0  # no film size: refused
 
 
 @pytest.mark.gpu
@@ -268,6 +308,41 @@ def test_group_film_equals_one_device(devices):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
+def test_queued_group_frames_equal_one_handle(devices):
+    """The queued group frame (rtg_group_render_async + rtg_group_reduce_async, bench.py's lean step
+    and the CLI's -gpus loop): four frames, each followed by a queued own-tile exchange with no host
+    wait, then the film; and a film read between frames sees exactly the frames before it. Both equal
+    one handle's waited-for renders of the same samples, bit for bit."""
+    from raytracingrenderer_amd import RayTracer, RayTracerGroup, loadScene
+    W, H = 160, 128  # 16 spp per frame: 328k paths, inside the frame pipeline's chunk limit
+    s = loadScene(os.path.join(SCENES, "cornell-box"), width=W, height=H)
+    ref = RayTracer(s, seed=23)
+    want = []
+    for k in range(4):
+        ref.render(16, first_sample=16 * k)
+        want.append(ref.film()[0])
+    g = RayTracerGroup(s, devices=devices, seed=23)
+    for k in range(4):
+        g.render(16, first_sample=16 * k, sync=False)
+        g.reduce(sync=False)
+    got, spp = g.film()
+    assert spp == 64
+    assert np.array_equal(got.view(np.uint32), want[3].view(np.uint32))
+    g.clear()
+    for k in range(4):
+        g.render(16, first_sample=16 * k, sync=False)
+        g.reduce(sync=False)
+        if k in (1, 2):
+            assert np.array_equal(g.film()[0].view(np.uint32), want[k].view(np.uint32)), k
+    g.synchronize()
+    assert g.reduce_ms() > 0.0
+    g.render(16, first_sample=64, sync=False)  # no exchange queued: film() runs one first
+    ref.render(16, first_sample=64)
+    assert np.array_equal(g.film()[0].view(np.uint32), ref.film()[0].view(np.uint32))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("opt", [["-gpus", "1"], ["-devices", "0,0,0"]])
 def test_cli_multi_gpu_output_equals_single(tmp_path, opt):
     """The CLI's multi-GPU mode (Main.cpp frame loop on rtg_group) writes the same result_<spp>.hdr
@@ -312,6 +387,12 @@ def test_group_over_distinct_devices_equals_one_device():
     g = RayTracerGroup(s, devices=[0, 1], seed=17)
     assert g.uses_rccl
     g.render(3, first_sample=0)
+    assert np.array_equal(g.film()[0].view(np.uint32), one.film()[0].view(np.uint32))
+    # queued frames and exchanges (the ranks' RCCL send/recv on the exchange streams)
+    g.clear()
+    for k in range(3):
+        g.render(1, first_sample=k, sync=False)
+        g.reduce(sync=False)
     assert np.array_equal(g.film()[0].view(np.uint32), one.film()[0].view(np.uint32))
 
 
