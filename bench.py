@@ -35,7 +35,11 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, same guide (§L2)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")  # rocprofv3 PMC passes of the C3 bench
+# rocprofv3 PMC passes of each config's bench line (tools/pmc_config.sh: FETCH_SIZE, WRITE_SIZE and
+# the DRAM share of L2 read requests, each its own run), per config; quoted only on the workload they
+# were taken on (the file's "spp", one GPU, the whole film)
+PMC_SUMMARIES = {c: os.path.join(ROOT, "profiles", "r06_pmc_traffic_%s.json" % c.lower()) for c in ("C2", "C3", "C4", "C5")}
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")  # round 5's C3 passes (fallback)
 KSTATS = os.path.join(ROOT, "profiles", "r05_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
 VALU_ISSUE = os.path.join(ROOT, "profiles", "r05_valu_issue.json")    # tools/valu_issue.py (SQ_INSTS_VALU passes)
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
@@ -452,11 +456,18 @@ def main():
     # the reference (extension_rays: one camera ray per sample) are what `value` is quoted on
     def traced_ext(st_):
         return st_["extension_rays"] - st_["paths"] + st_["traced_camera_rays"]
+    # bytes the walk itself fetches per counting pass: a 64-B node record per node step (wide or BVH2),
+    # a triangle's first 32 B per test and its last 16 B when its plane distance is a candidate, a 32-B
+    # leaf box per candidate hit, and 48 B of ray I/O per ray (origin + direction in, result out)
+    fetched = (64.0 * cw["node_lane_steps"] + 32.0 * (cw["tri_tests"] + cw["shadow_tri_tests"])
+               + 16.0 * cw["tri_tail_loads"] + 32.0 * cw["leafbox_tests"] + 48.0 * (traced_ext(cw) + cw["shadow_rays"]))
     totals = np.array([ext_rays, shadow_rays, paths, extend_ms, extend_launches,
                        cs["node_visits"], cs["tri_tests"], traced_ext(cs),
                        cw["node_visits"], cw["tri_tests"],
                        cs["shadow_node_visits"], cs["shadow_tri_tests"], cs["shadow_rays"],
-                       ext_rays - paths + cam_traced], dtype=np.float64)
+                       ext_rays - paths + cam_traced,
+                       traced_ext(cw), cw["shadow_node_visits"], cw["shadow_tri_tests"], cw["shadow_rays"], fetched],
+                      dtype=np.float64)
     t_max = elapsed
     if world > 1:
         import torch
@@ -467,7 +478,7 @@ def main():
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         t_max = float(te.item())
     (ext_rays, shadow_rays, paths, extend_ms, extend_launches, c_nodes, c_tris, c_ext, w_nodes, w_tris,
-     s_nodes, s_tris, c_sh, ext_traced) = totals.tolist()
+     s_nodes, s_tris, c_sh, ext_traced, w_ext, ws_nodes, ws_tris, w_sh, w_fetched) = totals.tolist()
     rays = ext_rays + shadow_rays
     rays_traced = ext_traced + shadow_rays
     mrays = rays / t_max / 1e6  # the reference's ray count (a camera ray per sample)
@@ -502,18 +513,27 @@ def main():
     req_step = (4.0 * cw["node_lane_steps"] + 2.0 * (cw["tri_tests"] + cw["shadow_tri_tests"])
                 + cw["tri_tail_loads"] + 2.0 * cw["leafbox_tests"] + REQ_PER_RAY_IO * all_rays)
     req_totals = np.array([req_step * n_steps, rec_step * n_steps], dtype=np.float64)
-    # SURVEY.md §8d algorithmic bytes B = 32 B x box tests + 36 B x triangle tests + 48 B ray I/O,
-    # with the box / triangle tests of the reference's own walk (BVH2, counted on the same workload);
-    # these bytes are served by L1/L2/Infinity Cache, so they are compared with the L2 bandwidth
-    boxes_per_ray = c_nodes / max(c_ext, 1)
-    tris_per_ray = c_tris / max(c_ext, 1)
+    # SURVEY.md §8d algorithmic bytes B_ray = 32 B x AABB tests + 36 B x triangle tests + 48 B ray I/O,
+    # "the AABB and triangle counts measured by the build's counting mode on the config's exact input":
+    # the box / triangle tests of the walk k_trace runs (the 4-wide tree's slot tests, triangle tests),
+    # counted on the same workload. These bytes are served by L1 / L2 / Infinity Cache (the hot scene
+    # is ~70 MB), so the peak they are held to is the L2 bandwidth.
+    boxes_per_ray = w_nodes / max(w_ext, 1)
+    tris_per_ray = w_tris / max(w_ext, 1)
     b_ray = 32.0 * boxes_per_ray + 36.0 * tris_per_ray + 48.0
-    s_boxes_per_ray = s_nodes / max(c_sh, 1)
-    s_tris_per_ray = s_tris / max(c_sh, 1)
+    s_boxes_per_ray = ws_nodes / max(w_sh, 1)
+    s_tris_per_ray = ws_tris / max(w_sh, 1)
     b_sray = 32.0 * s_boxes_per_ray + 36.0 * s_tris_per_ray + 48.0
     # time and rays both summed over ranks and launches
-    # (per traced ray: the counting pass's box / triangle tests over its traced rays)
     algo_gbs = (b_ray * ext_traced + b_sray * shadow_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
+    # the same formula with the reference's own BVH2 walk's counts (rounds 1-5's headline): the bytes
+    # RTBase's traversal would test, not what this walk fetches
+    r_b_ray = 32.0 * c_nodes / max(c_ext, 1) + 36.0 * c_tris / max(c_ext, 1) + 48.0
+    r_b_sray = 32.0 * s_nodes / max(c_sh, 1) + 36.0 * s_tris / max(c_sh, 1) + 48.0
+    ref_gbs = (r_b_ray * ext_traced + r_b_sray * shadow_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
+    # the bytes this walk requests (node records, triangle heads / tails, leaf boxes, ray I/O)
+    fetched_per_ray = w_fetched / max(w_ext + w_sh, 1)
+    fetched_gbs = fetched_per_ray * (ext_traced + shadow_rays) / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
     if world > 1:
         import torch
         rt_ = torch.tensor(req_totals, dtype=torch.float64, device=coll_dev)
@@ -523,17 +543,23 @@ def main():
     achieved_rec = req_totals[1] / (extend_ms / 1e3) / 1e9 if extend_ms > 0 else None
     ceiling = request_ceiling(scene.desc.n_tris)
     avg_launch_s = extend_ms / max(extend_launches, 1) / 1e3
-    # profiles/ evidence for the profiled workload (C3, 64 spp, one GPU): PMC traffic, kernel-trace
-    # durations, and the locality-matched replay ceiling; other configs / shards / N > 1 report null
+    # profiles/ evidence for the profiled workloads (each config's bench line, one GPU, the whole film):
+    # PMC traffic and kernel-trace durations; other shapes / shards / N > 1 report null
     traffic = pmc = None
-    profiled = (a.config == "C3" and world == 1 and group_devs is None and a.shard_of <= 1 and a.spp == 64 and a.tris == 1_000_000
-                and (a.width, a.height) == (1024, 1024) and a.max_depth == 4)
-    if profiled and os.path.exists(PMC_SUMMARY):
+    pmc_path = None
+    c_def = CONFIGS[a.config]
+    profiled = (world == 1 and group_devs is None and a.shard_of <= 1 and a.tris == 1_000_000
+                and (a.width, a.height) == (c_def["width"], c_def["height"]) and a.max_depth == c_def["depth"])
+    for path in (PMC_SUMMARIES[a.config],) + ((PMC_SUMMARY,) if a.config == "C3" else ()):
+        if not profiled or pmc is not None or not os.path.exists(path):
+            continue
         try:
-            pmc = json.load(open(PMC_SUMMARY))
-            traffic = pmc.get("extend_hbm_bytes_per_launch")
+            pj = json.load(open(path))
         except Exception:
-            pmc = None
+            continue
+        if pj.get("spp", 64 if path == PMC_SUMMARY else None) == a.spp:
+            pmc, pmc_path = pj, path
+            traffic = pj.get("extend_hbm_bytes_per_launch")
     replay = None
     # (a rank of N renders rank 0's share of an N-way split up to the diagonal offset: shard-of N's ceiling)
     replay_file = ROOF_REPLAYS.get((a.config, max(a.shard_of, world, 1))) if group_devs is None else None
@@ -562,7 +588,7 @@ def main():
 
     # VALU issue of the two hot kernels against the chip's wave64 issue peak (C3 PMC passes, profiles/)
     valu = {}
-    if profiled and os.path.exists(VALU_ISSUE):
+    if profiled and a.config == "C3" and a.spp == 64 and os.path.exists(VALU_ISSUE):
         try:
             vj = json.load(open(VALU_ISSUE))
             for key, name in (("trace", "k_trace<false, false>"), ("shade", "k_shade<false, ...>")):
@@ -622,31 +648,47 @@ def main():
                                        % (world, "RCCL" if backend == "nccl" else backend) if world > 1 else
                                        "one GPU rendering rank 0's tiles of %d (shard-of diagnostic, no exchange)" % a.shard_of
                                        if a.shard_of > 1 else "one GPU, every tile (no exchange)")},
-            # headline roofline: a hardware peak. SURVEY.md 8d's algorithmic bytes of k_trace per
-            # launch / its average launch time, against the L2 aggregate bandwidth that serves them
-            # (they exceed the HBM peak: the ~70 MB hot scene lives in L2 + Infinity Cache, and the
-            # PMC-measured HBM bytes are `traffic`). The walk's limiter, dependent random record
-            # fetches, is priced in `fetches` against a microbenchmark and a replay of its own stream.
+            # headline roofline: a hardware peak. SURVEY.md 8d's algorithmic bytes of k_trace (with the
+            # box / triangle tests of the walk it runs) per launch / its average launch time, against
+            # the L2 aggregate bandwidth that serves them (the ~70 MB hot scene lives in L2 + Infinity
+            # Cache; the PMC-measured HBM bytes are `traffic`). frac_hw: the bytes the walk actually
+            # requests (node records, triangle heads and tails, leaf boxes, ray I/O) against the same
+            # peak. The walk's limiter, dependent random record fetches, is priced in `fetches`.
             "roofline": {"bound": "l2", "kernel": "k_trace (extension + shadow rays)",
                          "achieved": None if algo_gbs is None else round(algo_gbs, 1),
                          "peak": L2_PEAK_GBS, "unit": "GB/s",
                          "frac": None if algo_gbs is None else round(algo_gbs / L2_PEAK_GBS, 4),
-                         "frac_hw": None if algo_gbs is None else round(algo_gbs / L2_PEAK_GBS, 4),
+                         "frac_hw": None if fetched_gbs is None else round(fetched_gbs / L2_PEAK_GBS, 4),
                          "peak_is": "MI355X aggregate L2 bandwidth, /opt/skills/guides/MI355X_MICROARCH.md (L2 per XCD)",
-                         "definition": ("SURVEY.md 8d: 32 B x box tests + 36 B x triangle tests + 48 B per ray, box / "
-                                        "triangle tests of the reference BVH2 walk counted on this workload; per launch "
-                                        "= bytes of the launch's rays / avg_launch_ms"),
+                         "definition": ("SURVEY.md 8d: 32 B x box tests + 36 B x triangle tests + 48 B per ray, with the "
+                                        "box (4-wide slot) and triangle tests of the walk k_trace runs, counted on this "
+                                        "workload by RTG_OPT_COUNT; per launch = bytes of the launch's rays / avg_launch_ms"),
                          "bytes_per_ray": round(b_ray, 1), "bytes_per_shadow_ray": round(b_sray, 1),
                          "box_tests_per_ray": round(boxes_per_ray, 2), "tri_tests_per_ray": round(tris_per_ray, 2),
                          "shadow_box_tests_per_ray": round(s_boxes_per_ray, 2),
                          "shadow_tri_tests_per_ray": round(s_tris_per_ray, 2),
-                         "frac_of_hbm_peak": None if algo_gbs is None else round(algo_gbs / HBM_PEAK_GBS, 4),
+                         "fetched": {"achieved": None if fetched_gbs is None else round(fetched_gbs, 1),
+                                     "bytes_per_ray": round(fetched_per_ray, 1),
+                                     "frac_of_l2_peak": None if fetched_gbs is None else round(fetched_gbs / L2_PEAK_GBS, 4),
+                                     "definition": "bytes the walk requests: 64 B per node step, 32 B per triangle test "
+                                                   "+ 16 B per triangle tail, 32 B per leaf box, 48 B of ray I/O per ray"},
+                         "reference_bvh2_bytes": {
+                             "achieved": None if ref_gbs is None else round(ref_gbs, 1),
+                             "bytes_per_ray": round(r_b_ray, 1), "bytes_per_shadow_ray": round(r_b_sray, 1),
+                             "box_tests_per_ray": round(c_nodes / max(c_ext, 1), 2),
+                             "tri_tests_per_ray": round(c_tris / max(c_ext, 1), 2),
+                             "ratio_to_l2_peak": None if ref_gbs is None else round(ref_gbs / L2_PEAK_GBS, 4),
+                             "ratio_to_hbm_peak": None if ref_gbs is None else round(ref_gbs / HBM_PEAK_GBS, 4),
+                             "why_not_a_fraction": ("the same 8d formula with the box / triangle tests of the reference's "
+                                                    "BVH2 walk (culled, counted by RTG_OPT_BVH2 on this workload): the bytes "
+                                                    "RTBase's traversal would test, not what k_trace fetches, so the rate can "
+                                                    "exceed a hardware peak (rounds 1-5 quoted it as the headline)")},
                          "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                          "traffic": traffic,
                          "traffic_source": (None if traffic is None else
                                             "%s: rocprofv3 PMC (FETCH_SIZE x1 for the gathers + WRITE_SIZE, DRAM share) "
                                             "of this workload in separate passes; from profiles/, not measured in this run"
-                                            % os.path.relpath(PMC_SUMMARY, ROOT)),
+                                            % os.path.relpath(pmc_path, ROOT)),
                          "hbm": {"bytes_per_launch": traffic,
                                  "achieved_gbs": round(traffic / avg_launch_s / 1e9, 1) if traffic and extend_ms > 0 else None,
                                  "peak_gbs": HBM_PEAK_GBS,
@@ -666,10 +708,13 @@ def main():
                                                                    "records, %d MiB table, %d VALU/step (microbenchmark)"
                                                                    % (os.path.relpath(ROOF_SWEEP, ROOT), ceiling["table_mib"],
                                                                       ceiling["valu_per_step"])}),
-                             "replay_ceiling": (None if not replay else
-                                                {"peak": round(replay["ceiling_g_fetches_per_s"], 1),
-                                                 "frac_vs_replay": (round(achieved_rec / replay["ceiling_g_fetches_per_s"], 4)
-                                                                    if achieved_rec and replay_shape_ok else None),
+                             # not a ceiling: the replay serialises each ray's captured fetches with 8
+                             # dependent VALU each; the walk overlaps parked-leaf triangle fetches with
+                             # node steps and runs faster than it on C3 and C4
+                             "replay_reference": (None if not replay else
+                                                {"rate": round(replay["ceiling_g_fetches_per_s"], 1),
+                                                 "ratio_vs_replay": (round(achieved_rec / replay["ceiling_g_fetches_per_s"], 4)
+                                                                     if achieved_rec and replay_shape_ok else None),
                                                  "chunk_spp": replay.get("chunk_spp"),
                                                  "matches_line_chunk": replay_shape_ok,
                                                  "k_trace_ms": round(replay["k_trace_ms"], 2),
@@ -678,8 +723,8 @@ def main():
                                                  "frac_at_measurement": round(replay["frac"], 4),
                                                  "source": ("this workload's own fetch stream captured and replayed with "
                                                             "nothing else in the loop (tools/roof_replay.py); read from %s, "
-                                                            "a stored profile, not measured in this run; self-referential: "
-                                                            "it keeps the walk's fetch count and locality"
+                                                            "a stored profile, not measured in this run; a reference rate, "
+                                                            "not a bound (the walk can run faster: ratio above 1)"
                                                             % os.path.relpath(replay_file, ROOT))}),
                              "requests": {"achieved": None if achieved_req is None else round(achieved_req, 1),
                                           "peak": None if ceiling is None else round(ceiling["g_req_per_s"], 1),
@@ -717,7 +762,7 @@ def main():
                                "pmc": shade_pmc,
                                "pmc_source": (None if shade_pmc is None else "%s (k_shade<false>, DRAM-level bytes "
                                               "FETCH_SIZE x2 + WRITE_SIZE per launch, rocprof kernel-trace duration); "
-                                              "from profiles/, not measured in this run" % os.path.relpath(PMC_SUMMARY, ROOT))},
+                                              "from profiles/, not measured in this run" % os.path.relpath(pmc_path, ROOT))},
             "kernel_ms_per_step_rank0": {"trace": round(local_kernel_ms[0] / a.steps, 2),
                                          "generate_shade_accumulate": round(local_kernel_ms[2] / a.steps, 2)},
             "timed_step": ("lean: queued renders (frame pipeline)%s, film cleared once before, ray counts read once "

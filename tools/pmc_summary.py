@@ -16,7 +16,7 @@ def per_kernel(path, counter):
             acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     return acc
 
-def main(fetch_csv, write_csv, stats_csv, out_json, dram_csv=None):
+def main(fetch_csv, write_csv, stats_csv, out_json, dram_csv=None, config=None, spp=None):
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
     rq = per_kernel(dram_csv, "TCC_EA0_RDREQ_sum") if dram_csv else {}
@@ -36,8 +36,16 @@ def main(fetch_csv, write_csv, stats_csv, out_json, dram_csv=None):
         if k in rq and sum(rq[k]) > 0:
             # share of L2 read requests that went to DRAM (the rest hit the Infinity Cache)
             out["kernels"][k]["dram_share_of_l2_read_requests"] = round(sum(rd.get(k, [0])) / sum(rq[k]), 4)
-    ext = [k for k in out["kernels"] if k.startswith("void k_trace<false>") or k.startswith("void k_trace<false, false>")]
+    if config:
+        out["config"] = config
+    if spp:
+        out["spp"] = int(spp)
+    # the traversal kernel of the bench (not the counting variant): k_trace<false, SMALL>, the one
+    # with the most kernel-trace time (the small-scene variant on C2)
+    ext = [k for k in out["kernels"] if k.startswith("void k_trace<false")]
+    ext.sort(key=lambda k: -(out["kernels"][k]["avg_ns_trace"] or 0) * (out["kernels"][k]["calls_trace"] or 0))
     if ext:
+        out["extend_kernel"] = ext[0]
         e = out["kernels"][ext[0]]
         out["extend_l2_fabric_bytes_per_launch"] = e["read_bytes_corrected"] + e["write_bytes"]
         share = e.get("dram_share_of_l2_read_requests")
@@ -47,4 +55,4 @@ def main(fetch_csv, write_csv, stats_csv, out_json, dram_csv=None):
     print(json.dumps(out, indent=1))
 
 if __name__ == "__main__":
-    main(*sys.argv[1:6])
+    main(*sys.argv[1:8])
