@@ -37,7 +37,7 @@ extern "C" {
  * 5: rtg_build_id; the own-tile film exchange (rtg_tile_pixels, rtg_film_gather, rtg_film_scatter),
  *    which rtg_group_reduce now uses in place of a whole-film ncclReduce; rtg_stats.chunk_samples
  * 6: rtg_group_render_async / rtg_group_reduce_async / rtg_group_synchronize (queued group frames);
- *    rtg_film_scatter takes the film's pixel count */
+ *    rtg_film_scatter takes the film's pixel count; rtg_stats.lane_idle_* appended */
 #define RTG_ABI_VERSION 6
 
 /* error codes */
@@ -131,6 +131,12 @@ typedef struct rtg_stats {
                                    /* extension_rays counts one per sample, as the reference casts them */
     uint64_t chunk_samples;        /* samples per pixel of the largest wavefront chunk issued since the */
                                    /* last rtg_clear (ABI 5): the chunk shape of the render           */
+    /* RTG_OPT_COUNT (ABI 6): lanes not stepping a node in a traversal loop iteration, by reason,   */
+    /* summed like node_lane_steps (lane_slots = node_lane_steps + these four)                      */
+    uint64_t lane_idle_no_ray;       /* no ray: waiting for the wave's refill                        */
+    uint64_t lane_idle_last_leaf;    /* walk done, its parked leaf waiting for the wave's leaf phase */
+    uint64_t lane_idle_leaf_blocked; /* reached a second leaf while one is parked                    */
+    uint64_t lane_idle_retiring;     /* ray finished, retired at the next iteration                  */
 } rtg_stats;
 
 typedef struct rtg_handle rtg_handle;

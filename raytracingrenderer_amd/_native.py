@@ -57,7 +57,9 @@ class rtg_stats(C.Structure):
                 ("lane_slots", C.c_uint64), ("node_lane_steps", C.c_uint64), ("leaf_lane_steps", C.c_uint64),
                 ("leaf_phase_slots", C.c_uint64), ("pops", C.c_uint64), ("cullable_pops", C.c_uint64),
                 ("tri_tail_loads", C.c_uint64), ("leafbox_tests", C.c_uint64), ("traced_camera_rays", C.c_uint64),
-                ("chunk_samples", C.c_uint64)]
+                ("chunk_samples", C.c_uint64), ("lane_idle_no_ray", C.c_uint64),
+                ("lane_idle_last_leaf", C.c_uint64), ("lane_idle_leaf_blocked", C.c_uint64),
+                ("lane_idle_retiring", C.c_uint64)]
 
 
 class rth_load_options(C.Structure):

@@ -15,6 +15,7 @@
 using namespace rtgd;
 
 #define RTG_TB 256          // threads per block (4 waves)
+#define RTG_NSTATS 20       // device counters behind rtg_stats (rtg_handle::d_stats)
 #ifndef RTG_TTB
 #define RTG_TTB 64          // threads per k_trace block: one wave, so a drained wave gives its CU slot
                             // back at once (256: C3 -0.4 %, shard-of 8 -0.6 %, profiles/r03_trace_block_ab.txt)

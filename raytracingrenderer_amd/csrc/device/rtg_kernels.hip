@@ -77,6 +77,9 @@ void k_trace(SceneView s, TraceIO io) {
     unsigned long long c_nodes = 0, c_tris = 0, c_snodes = 0, c_stris = 0, c_slots = 0, c_nstep = 0, c_lstep = 0,
                        c_cullpop = 0, c_pops = 0, c_lslots = 0, c_lbox = 0;
     unsigned c_tails = 0;  // triangle records whose last 16 B were fetched (COUNT)
+    // COUNT: why a lane is not stepping a node in an iteration: no ray, its walk done but its parked
+    // leaf not run yet, a second leaf reached while one is parked, retiring this iteration
+    unsigned long long c_idle_e = 0, c_idle_ll = 0, c_idle_lb = 0, c_idle_r = 0;
     unsigned pool_base = 0, pool_left = 0, last_b = 0;  // wave-uniform
     const unsigned tail_rays = (gthreads / 64u) * (unsigned)RTG_FETCH * RTG_FETCH_TAIL / (io.fetch8 ? 8u : 1u);
     // the 8 slices (trace_slice) in LDS, read when a wave fetches work: the loop keeps only the
@@ -218,6 +221,10 @@ void k_trace(SceneView s, TraceIO io) {
         if (COUNT) {
             c_slots += 64;
             c_nstep += (have && cur >= 0) ? 1 : 0;
+            c_idle_e += !have ? 1 : 0;
+            c_idle_ll += (have && cur == RTG_EXIT && pend != RTG_EXIT) ? 1 : 0;
+            c_idle_lb += (have && cur < 0 && cur != RTG_EXIT && pend != RTG_EXIT) ? 1 : 0;
+            c_idle_r += (have && cur == RTG_EXIT && pend == RTG_EXIT) ? 1 : 0;
         }
         if (!have || (cur == RTG_EXIT && pend == RTG_EXIT)) continue;
         // Leaf: the reference's leaf loop (Geometry.h:420-431 / 446-458) over 1-2 triangles (a wide
@@ -438,6 +445,10 @@ void k_trace(SceneView s, TraceIO io) {
             c_pops += __shfl_down(c_pops, off);
             c_lbox += __shfl_down(c_lbox, off);
             c_tails += __shfl_down(c_tails, off);
+            c_idle_e += __shfl_down(c_idle_e, off);
+            c_idle_ll += __shfl_down(c_idle_ll, off);
+            c_idle_lb += __shfl_down(c_idle_lb, off);
+            c_idle_r += __shfl_down(c_idle_r, off);
         }
         if (lane == 0) {
             atomicAdd(&io.stats[0], c_nodes);
@@ -452,6 +463,10 @@ void k_trace(SceneView s, TraceIO io) {
             atomicAdd(&io.stats[12], c_pops);
             atomicAdd(&io.stats[6], (unsigned long long)c_tails);
             atomicAdd(&io.stats[7], c_lbox);
+            atomicAdd(&io.stats[15], c_idle_e);
+            atomicAdd(&io.stats[16], c_idle_ll);
+            atomicAdd(&io.stats[17], c_idle_lb);
+            atomicAdd(&io.stats[18], c_idle_r);
         }
     }
 }
@@ -1509,8 +1524,8 @@ int upload_scene(int device, const HostScene& hs, rtg_handle* h) {
     HIPOK(hipMalloc((void**)&h->d_film, (size_t)h->W * h->H * 3 * sizeof(float)));
     HIPOK(hipMemset(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float)));
     HIPOK(hipMalloc((void**)&h->d_qctr, 4 * sizeof(unsigned)));
-    HIPOK(hipMalloc((void**)&h->d_stats, 16 * sizeof(unsigned long long)));
-    HIPOK(hipMemset(h->d_stats, 0, 16 * sizeof(unsigned long long)));
+    HIPOK(hipMalloc((void**)&h->d_stats, RTG_NSTATS * sizeof(unsigned long long)));
+    HIPOK(hipMemset(h->d_stats, 0, RTG_NSTATS * sizeof(unsigned long long)));
     for (auto& e : h->ev) HIPOK(hipEventCreate(&e));
 
     int occ = 0;
@@ -2265,7 +2280,7 @@ int rtg_clear(rtg_handle* h) {
     h->pend_n = 0;  // queued calls not issued yet: the clear would zero what they add
     if (int rc = join_frames(h)) return rc;
     HIPOK(hipMemsetAsync(h->d_film, 0, (size_t)h->W * h->H * 3 * sizeof(float), h->stream));
-    HIPOK(hipMemsetAsync(h->d_stats, 0, 16 * sizeof(unsigned long long), h->stream));
+    HIPOK(hipMemsetAsync(h->d_stats, 0, RTG_NSTATS * sizeof(unsigned long long), h->stream));
     HIPOK(hipStreamSynchronize(h->stream));
     h->spp = 0;
     h->stats = rtg_stats{};
@@ -2277,7 +2292,7 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     HIPOK(hipSetDevice(h->device));
     if (int rc = join_frames(h)) return rc;
     HIPOK(hipStreamSynchronize(h->stream));
-    unsigned long long c[16] = {};
+    unsigned long long c[RTG_NSTATS] = {};
     HIPOK(hipMemcpy(c, h->d_stats, sizeof(c), hipMemcpyDeviceToHost));
     h->stats.node_visits = c[0];
     h->stats.tri_tests = c[1];
@@ -2294,6 +2309,10 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     h->stats.tri_tail_loads = c[6];
     h->stats.leafbox_tests = c[7];
     h->stats.traced_camera_rays = c[14];
+    h->stats.lane_idle_no_ray = c[15];
+    h->stats.lane_idle_last_leaf = c[16];
+    h->stats.lane_idle_leaf_blocked = c[17];
+    h->stats.lane_idle_retiring = c[18];
     *out = h->stats;
     return RTG_OK;
 }
