@@ -37,6 +37,12 @@ using namespace rtgd;
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
 #endif
+#ifndef RTG_LEAF_MINWALK
+#define RTG_LEAF_MINWALK 0  // ... or once at most this many lanes can take a node step
+#endif
+#ifndef RTG_LEAF_SWAP
+#define RTG_LEAF_SWAP 0     // 1: a lane reaching a second leaf swaps it with its stack top and walks on
+#endif
 #ifndef RTG_REFILL
 #define RTG_REFILL 12       // refill idle lanes once at least this many are idle (the setup code then
                             // runs with more lanes per execution)
