@@ -748,7 +748,7 @@ def main():
                                                  round(cw["leaf_phase_slots"] / max(cw["lane_slots"], 1), 3)],
                          # the lanes not stepping a node, by reason, as fractions of lane_slots
                          "lane_idle_node": {k: round(cw.get("lane_idle_" + k, 0) / max(cw["lane_slots"], 1), 4)
-                                            for k in ("no_ray", "last_leaf", "leaf_blocked", "retiring")}},
+                                            for k in ("no_ray", "last_leaf", "leaf_blocked", "retiring", "leaf_popped")}},
             "roofline_shade": {"bound": "hbm", "kernel": "k_shade (+ k_generate, k_accumulate in the time)",
                                "achieved": None if shade_algo_gbs is None else round(shade_algo_gbs, 1),
                                "peak": HBM_PEAK_GBS, "unit": "GB/s",

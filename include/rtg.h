@@ -132,11 +132,12 @@ typedef struct rtg_stats {
     uint64_t chunk_samples;        /* samples per pixel of the largest wavefront chunk issued since the */
                                    /* last rtg_clear (ABI 5): the chunk shape of the render           */
     /* RTG_OPT_COUNT (ABI 6): lanes not stepping a node in a traversal loop iteration, by reason,   */
-    /* summed like node_lane_steps (lane_slots = node_lane_steps + these four)                      */
+    /* summed like node_lane_steps (lane_slots = node_lane_steps + these five)                      */
     uint64_t lane_idle_no_ray;       /* no ray: waiting for the wave's refill                        */
     uint64_t lane_idle_last_leaf;    /* walk done, its parked leaf waiting for the wave's leaf phase */
     uint64_t lane_idle_leaf_blocked; /* reached a second leaf while one is parked                    */
     uint64_t lane_idle_retiring;     /* ray finished, retired at the next iteration                  */
+    uint64_t lane_idle_leaf_popped;  /* popped a leaf last iteration; parked in this one             */
 } rtg_stats;
 
 typedef struct rtg_handle rtg_handle;

@@ -59,7 +59,7 @@ class rtg_stats(C.Structure):
                 ("tri_tail_loads", C.c_uint64), ("leafbox_tests", C.c_uint64), ("traced_camera_rays", C.c_uint64),
                 ("chunk_samples", C.c_uint64), ("lane_idle_no_ray", C.c_uint64),
                 ("lane_idle_last_leaf", C.c_uint64), ("lane_idle_leaf_blocked", C.c_uint64),
-                ("lane_idle_retiring", C.c_uint64)]
+                ("lane_idle_retiring", C.c_uint64), ("lane_idle_leaf_popped", C.c_uint64)]
 
 
 class rth_load_options(C.Structure):

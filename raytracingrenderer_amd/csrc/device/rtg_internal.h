@@ -15,7 +15,7 @@
 using namespace rtgd;
 
 #define RTG_TB 256          // threads per block (4 waves)
-#define RTG_NSTATS 20       // device counters behind rtg_stats (rtg_handle::d_stats)
+#define RTG_NSTATS 24       // device counters behind rtg_stats (rtg_handle::d_stats)
 #ifndef RTG_TTB
 #define RTG_TTB 64          // threads per k_trace block: one wave, so a drained wave gives its CU slot
                             // back at once (256: C3 -0.4 %, shard-of 8 -0.6 %, profiles/r03_trace_block_ab.txt)
@@ -39,6 +39,9 @@ using namespace rtgd;
 #endif
 #ifndef RTG_LEAF_MINWALK
 #define RTG_LEAF_MINWALK 0  // ... or once at most this many lanes can take a node step
+#endif
+#ifndef RTG_POP_PARK
+#define RTG_POP_PARK 0      // 1: a popped leaf is parked at once (one more pop) when no leaf is parked
 #endif
 #ifndef RTG_LEAF_SWAP
 #define RTG_LEAF_SWAP 0     // 1: a lane reaching a second leaf swaps it with its stack top and walks on

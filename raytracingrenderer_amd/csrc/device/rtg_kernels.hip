@@ -78,8 +78,9 @@ void k_trace(SceneView s, TraceIO io) {
                        c_cullpop = 0, c_pops = 0, c_lslots = 0, c_lbox = 0;
     unsigned c_tails = 0;  // triangle records whose last 16 B were fetched (COUNT)
     // COUNT: why a lane is not stepping a node in an iteration: no ray, its walk done but its parked
-    // leaf not run yet, a second leaf reached while one is parked, retiring this iteration
-    unsigned long long c_idle_e = 0, c_idle_ll = 0, c_idle_lb = 0, c_idle_r = 0;
+    // leaf not run yet, a second leaf reached while one is parked, retiring this iteration, a leaf
+    // popped last iteration (parked in this one)
+    unsigned long long c_idle_e = 0, c_idle_ll = 0, c_idle_lb = 0, c_idle_r = 0, c_idle_lp = 0;
     unsigned pool_base = 0, pool_left = 0, last_b = 0;  // wave-uniform
     const unsigned tail_rays = (gthreads / 64u) * (unsigned)RTG_FETCH * RTG_FETCH_TAIL / (io.fetch8 ? 8u : 1u);
     // the 8 slices (trace_slice) in LDS, read when a wave fetches work: the loop keeps only the
@@ -225,6 +226,7 @@ void k_trace(SceneView s, TraceIO io) {
             c_idle_ll += (have && cur == RTG_EXIT && pend != RTG_EXIT) ? 1 : 0;
             c_idle_lb += (have && cur < 0 && cur != RTG_EXIT && pend != RTG_EXIT) ? 1 : 0;
             c_idle_r += (have && cur == RTG_EXIT && pend == RTG_EXIT) ? 1 : 0;
+            c_idle_lp += (have && cur < 0 && cur != RTG_EXIT && pend == RTG_EXIT) ? 1 : 0;
         }
         if (!have || (cur == RTG_EXIT && pend == RTG_EXIT)) continue;
         // Leaf: the reference's leaf loop (Geometry.h:420-431 / 446-458) over 1-2 triangles (a wide
@@ -422,6 +424,20 @@ void k_trace(SceneView s, TraceIO io) {
                 if (COUNT && !anyr && sp < STK && kstk[sp][tid] > tbest) c_cullpop += 1;
                 if (sp >= STK) cur = io.ovf[(size_t)(sp - STK) * gthreads + gtid];
             }
+#if RTG_POP_PARK
+            // a popped leaf with no leaf parked: park it now and pop once more, so the lane has a
+            // node for the next iteration's step instead of spending that iteration parking
+            if (cur < 0 && cur != RTG_EXIT && pend == RTG_EXIT) {
+                pend = cur;
+                if (sp == 0) {
+                    cur = RTG_EXIT;
+                } else {
+                    --sp;
+                    cur = stk[sp < STK ? sp : 0][tid];
+                    if (sp >= STK) cur = io.ovf[(size_t)(sp - STK) * gthreads + gtid];
+                }
+            }
+#endif
         }
         // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on, or (the queue is
         // dry) any parked leaf: the drain is latency-bound, lanes should not wait for each other
@@ -458,6 +474,7 @@ void k_trace(SceneView s, TraceIO io) {
             c_idle_ll += __shfl_down(c_idle_ll, off);
             c_idle_lb += __shfl_down(c_idle_lb, off);
             c_idle_r += __shfl_down(c_idle_r, off);
+            c_idle_lp += __shfl_down(c_idle_lp, off);
         }
         if (lane == 0) {
             atomicAdd(&io.stats[0], c_nodes);
@@ -476,6 +493,7 @@ void k_trace(SceneView s, TraceIO io) {
             atomicAdd(&io.stats[16], c_idle_ll);
             atomicAdd(&io.stats[17], c_idle_lb);
             atomicAdd(&io.stats[18], c_idle_r);
+            atomicAdd(&io.stats[19], c_idle_lp);
         }
     }
 }
@@ -2322,6 +2340,7 @@ int rtg_get_stats(rtg_handle* h, rtg_stats* out) {
     h->stats.lane_idle_last_leaf = c[16];
     h->stats.lane_idle_leaf_blocked = c[17];
     h->stats.lane_idle_retiring = c[18];
+    h->stats.lane_idle_leaf_popped = c[19];
     *out = h->stats;
     return RTG_OK;
 }

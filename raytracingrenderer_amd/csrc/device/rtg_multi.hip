@@ -36,6 +36,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -399,7 +400,8 @@ int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* de
                 g->h[r]->mem_cap = std::max<size_t>(1, freeb / 2 / (size_t)k);
         }
     }
-    if (g->distinct) {
+    // (A/B, round 6: RTG_GROUP_NO_RCCL1=1 forms no communicator for a group of one device)
+    if (g->distinct && (n_devices > 1 || !std::getenv("RTG_GROUP_NO_RCCL1"))) {
         if (!load_rccl()) {
             rtg_group_destroy(g);
             return RTG_ERR_HIP;

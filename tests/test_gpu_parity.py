@@ -845,7 +845,8 @@ def test_reference_side_binding_renders_reference_film(case):
 def test_handle_churn_with_queued_frames():
     """Many handles created, rendering (waited-for and queued, one chunk at a time and several) and
     destroyed in one process, as this suite does: destroying full-CU-mask streams deadlocked the HIP
-    runtime within a few handles (ROCm 7.2), so the slot streams are pooled per device."""
+    runtime within a few handles (ROCm 7.2), so the slot streams are plain streams of one priority
+    each, created and destroyed with their handle."""
     s = loadScene(os.path.join(SCENES, "cornell-mat"), width=64, height=35)
     want = gpu_film(s, 3, seed=7, max_depth=8)
     for i in range(60):
