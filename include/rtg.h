@@ -319,6 +319,9 @@ int  rtg_get_stats(rtg_handle* h, rtg_stats* out);
 /* Per traversal launch (k_trace) device time of the last render with RTG_OPT_TIMING, in launch
  * order (chunk by chunk, bounce by bounce): n receives the count, at most max are written. */
 int  rtg_launch_times(rtg_handle* h, double* trace_ms, uint32_t max, uint32_t* n);
+/* The rays each trace launch of the last timed render's last chunk walked (path tracer: launch b =
+ * bounce b's extension rays + bounce b-1's shadow rays; launch 0 the camera rays, one per pixel). */
+int  rtg_launch_rays(rtg_handle* h, uint64_t* rays, uint32_t max, uint32_t* n);
 /* Diagnostics of the locality-matched roofline (builds with RTG_DEBUG=1 only; RTG_ERR_ARG
  * otherwise). rtg_debug_capture(h, b): the next render records every record fetch of trace launch
  * b of its first chunk, per ray in order (-1: off). rtg_debug_replay(h, out[4]) replays that

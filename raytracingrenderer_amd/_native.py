@@ -97,6 +97,7 @@ RTG_EXPORTS = [
     ("rtg_clear", C.c_int, [C.c_void_p]),
     ("rtg_get_stats", C.c_int, [C.c_void_p, C.POINTER(rtg_stats)]),
     ("rtg_launch_times", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_uint32, u32p]),
+    ("rtg_launch_rays", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint32, u32p]),
     ("rtg_debug_capture", C.c_int, [C.c_void_p, C.c_int]),
     ("rtg_debug_replay", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     ("rtg_trace_closest", C.c_int, [C.c_void_p, f32p, C.c_uint32, f32p]),

@@ -33,6 +33,9 @@ using namespace rtgd;
 #ifndef RTG_SMALL_F4
 #define RTG_SMALL_F4 224    // small-scene image limit, float4s (3.5 KB): 11 x 256 B of stack + 3.5 KB per
 #endif                      // one-wave block keeps 24 blocks per CU in the 160 KB of LDS
+#ifndef RTG_SMALL_LB
+#define RTG_SMALL_LB 1      // the small-scene image holds the leaf boxes too (0: they stay in global memory)
+#endif
 #ifndef RTG_POSTPONE
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
@@ -320,6 +323,7 @@ struct rtg_handle {
     unsigned* d_cap_rays = nullptr;   // [2]: its extension and shadow ray counts
     unsigned cap_n = 0;               // rays the capture buffers hold
     std::vector<double> launch_ms;    // per trace launch of the last timed render (RTG_OPT_TIMING)
+    std::vector<unsigned long long> launch_rays;  // rays of each trace launch of its last chunk
     uint32_t bvh_depth = 0;
     SceneView sv{};
     DevCamera cam{};

@@ -100,7 +100,7 @@ void k_trace(SceneView s, TraceIO io) {
         for (int i = tid; i < s.img_n4; i += RTG_TTB) s_img[i] = s.img[i];
     __syncthreads();
     const DevTri48* tris = SMALL ? reinterpret_cast<const DevTri48*>(s_img + s.img_tri) : s.tris48;
-    const float4* lboxes = SMALL ? s_img + s.img_lb : s.leafbox;
+    const float4* lboxes = (SMALL && RTG_SMALL_LB) ? s_img + s.img_lb : s.leafbox;
     int slice = io.fetch8 ? (int)(blockIdx.x & 7u) : 0, tried = 0;  // wave-uniform
     unsigned s_len = __builtin_amdgcn_readfirstlane(s_tab[2][slice]);
     bool drained = false;                   // wave-uniform
@@ -1362,7 +1362,8 @@ int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
             leafbox[2 * (size_t)t + 1] = make_float4(b[4], b[5], 0.0f, 0.0f);
         }
     }
-    const bool small = hs.usew && nodesq.size() * 4 + (size_t)nt * 5 <= RTG_SMALL_F4;
+    // (RTG_SMALL_LB 0: the leaf boxes stay in global memory, read once per candidate hit)
+    const bool small = hs.usew && nodesq.size() * 4 + (size_t)nt * (RTG_SMALL_LB ? 5 : 3) <= RTG_SMALL_F4;
     float scale = 0.0f;
     for (int k = 0; k < 6; ++k) {
         float v = std::fabs(d->node_bounds[k]);
@@ -1375,7 +1376,7 @@ int prepare_scene(const rtg_scene_desc* d, HostScene& hs) {
         hs.img_tri = (int)hs.img.size();
         for (const DevTri48& t : tris48) hs.img.insert(hs.img.end(), {t.a, t.b, t.c});
         hs.img_lb = (int)hs.img.size();
-        hs.img.insert(hs.img.end(), leafbox.begin(), leafbox.begin() + (size_t)nt * 2);
+        if (RTG_SMALL_LB) hs.img.insert(hs.img.end(), leafbox.begin(), leafbox.begin() + (size_t)nt * 2);
     }
     // ---- materials, textures, lights
     std::vector<DevMat> mats(d->n_materials);
@@ -2025,6 +2026,21 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
         h->stats.extend_ms = h->stats.shadow_ms = h->stats.shade_ms = 0;
         h->stats.extend_launches = 0;
         h->launch_ms.clear();
+        // the rays of each trace launch of the last chunk (camera rays, then extension + shadow rays)
+        h->launch_rays.clear();
+        std::vector<Counters> cc((size_t)maxb + 1);
+        // (a waited-for render runs its chunks in slot 0)
+        if (h->slot[0].pb.ctr &&
+            hipMemcpy(cc.data(), h->slot[0].pb.ctr, cc.size() * sizeof(Counters), hipMemcpyDeviceToHost) == hipSuccess) {
+            for (int b = 0; b <= maxb; ++b) {
+                unsigned long long r = b == 0 ? cc[0].n_cam : 0ull;
+                for (int k = 0; k < 8; ++k) {
+                    if (b > 0 && b < maxb) r += cc[b].ne8[32 * k];
+                    if (b > 0) r += cc[b - 1].ns8[32 * k];
+                }
+                h->launch_rays.push_back(r);
+            }
+        }
         for (size_t j = 0; j < kinds.size(); ++j) {
             float ms = 0;
             (void)hipEventElapsedTime(&ms, h->kev[2 * j], h->kev[2 * j + 1]);
@@ -2196,6 +2212,13 @@ int rtg_launch_times(rtg_handle* h, double* trace_ms, uint32_t max, uint32_t* n)
     if (!h || !n) return RTG_ERR_ARG;
     *n = (uint32_t)h->launch_ms.size();
     for (uint32_t i = 0; trace_ms && i < std::min<uint32_t>(max, *n); ++i) trace_ms[i] = h->launch_ms[i];
+    return RTG_OK;
+}
+
+int rtg_launch_rays(rtg_handle* h, uint64_t* rays, uint32_t max, uint32_t* n) {
+    if (!h || !n) return RTG_ERR_ARG;
+    *n = (uint32_t)h->launch_rays.size();
+    for (uint32_t i = 0; rays && i < std::min<uint32_t>(max, *n); ++i) rays[i] = h->launch_rays[i];
     return RTG_OK;
 }
 
