@@ -34,7 +34,10 @@ using namespace rtgd;
 #define RTG_SMALL_F4 224    // small-scene image limit, float4s (3.5 KB): 11 x 256 B of stack + 3.5 KB per
 #endif                      // one-wave block keeps 24 blocks per CU in the 160 KB of LDS
 #ifndef RTG_SMALL_LB
-#define RTG_SMALL_LB 1      // the small-scene image holds the leaf boxes too (0: they stay in global memory)
+#define RTG_SMALL_LB 0      // 1: the small-scene image holds the leaf boxes too; 0: they stay in global
+#endif                      // memory, read once per candidate hit (C2 +4.8 %: cornell's SBVH image then fits)
+#ifndef RTG_CAM_GRID
+#define RTG_CAM_GRID 0      // 1: the camera launch runs at most one one-wave block per 64 rays
 #endif
 #ifndef RTG_POSTPONE
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
@@ -426,7 +429,8 @@ int join_frames(rtg_handle* h);
 // k_generate for the paths of a (camera rays at pixel centres, Scene.h:43-54)
 int launch_generate(rtg_handle* h, const ChunkArgs& a, const PathBufs& pb, hipStream_t st);
 // one k_trace launch (closest-hit rays of io.queue and any-hit rays of io.squeue) on stream st
-int launch_trace(rtg_handle* h, const TraceIO& io, hipStream_t st);
+// (max_blocks != 0: at most that many one-wave blocks instead of the resident grid)
+int launch_trace(rtg_handle* h, const TraceIO& io, hipStream_t st, unsigned max_blocks = 0);
 // rtg_shade.hip: one k_shade launch of `grid` blocks (ALT = alt, TAB = tab) for bounce b
 int launch_shade(bool alt, bool tab, unsigned grid, hipStream_t st, const SceneView& s, const ChunkArgs& a,
                  const PathBufs& p, int b);

@@ -427,7 +427,8 @@ void k_trace(SceneView s, TraceIO io) {
 #if RTG_POP_PARK
             // a popped leaf with no leaf parked: park it now and pop once more, so the lane has a
             // node for the next iteration's step instead of spending that iteration parking
-            if (cur < 0 && cur != RTG_EXIT && pend == RTG_EXIT) {
+            // (RTG_POP_PARK 2: the small-scene variant only)
+            if ((RTG_POP_PARK == 1 || SMALL) && cur < 0 && cur != RTG_EXIT && pend == RTG_EXIT) {
                 pend = cur;
                 if (sp == 0) {
                     cur = RTG_EXIT;
@@ -1683,12 +1684,13 @@ int launch_generate(rtg_handle* h, const ChunkArgs& a, const PathBufs& pb, hipSt
     return RTG_OK;
 }
 
-int launch_trace(rtg_handle* h, const TraceIO& io, hipStream_t st) {
+int launch_trace(rtg_handle* h, const TraceIO& io, hipStream_t st, unsigned max_blocks) {
     const bool small = h->sv.img != nullptr;
-    if (h->count && small) hipLaunchKernelGGL((k_trace<true, true>), dim3(h->trace_blocks_small_count), dim3(RTG_TTB), 0, st, h->sv, io);
-    else if (h->count) hipLaunchKernelGGL((k_trace<true, false>), dim3(h->trace_blocks_count), dim3(RTG_TTB), 0, st, h->sv, io);
-    else if (small) hipLaunchKernelGGL((k_trace<false, true>), dim3(h->trace_blocks_small), dim3(RTG_TTB), 0, st, h->sv, io);
-    else hipLaunchKernelGGL((k_trace<false, false>), dim3(h->trace_blocks), dim3(RTG_TTB), 0, st, h->sv, io);
+    auto g = [&](int full) { return dim3(max_blocks ? std::min<unsigned>((unsigned)full, max_blocks) : (unsigned)full); };
+    if (h->count && small) hipLaunchKernelGGL((k_trace<true, true>), g(h->trace_blocks_small_count), dim3(RTG_TTB), 0, st, h->sv, io);
+    else if (h->count) hipLaunchKernelGGL((k_trace<true, false>), g(h->trace_blocks_count), dim3(RTG_TTB), 0, st, h->sv, io);
+    else if (small) hipLaunchKernelGGL((k_trace<false, true>), g(h->trace_blocks_small), dim3(RTG_TTB), 0, st, h->sv, io);
+    else hipLaunchKernelGGL((k_trace<false, false>), g(h->trace_blocks), dim3(RTG_TTB), 0, st, h->sv, io);
     LAUNCH_OK("k_trace");
     return RTG_OK;
 }
@@ -1977,7 +1979,12 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
             timed_begin(h, ss, k);
             {
                 RoctxRange r_trace(roctx_stage_name(0, b));
-                if ((rc = launch_trace(h, io, ss))) return rc;
+                // the camera launch (a ray per pixel, one work counter): with RTG_CAM_GRID, no more
+                // one-wave blocks than it has tail batches of rays, so waves without work do not
+                // queue their probes on the counter
+                const unsigned cam_blocks = (RTG_CAM_GRID && b == 0)
+                                                ? std::max(8u, (a.npix + RTG_TAIL_BATCH - 1) / RTG_TAIL_BATCH) : 0u;
+                if ((rc = launch_trace(h, io, ss, cam_blocks))) return rc;
             }
             timed_end(h, ss, k); kinds.push_back(0); ++k;
             if (io.hcnt) HIPOK(hipEventRecord(h->tev[b], ss));
