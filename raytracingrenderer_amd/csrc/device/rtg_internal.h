@@ -37,8 +37,8 @@ using namespace rtgd;
 #define RTG_SMALL_LB 0      // 1: the small-scene image holds the leaf boxes too; 0: they stay in global
 #endif                      // memory, read once per candidate hit (C2 +4.8 %: cornell's SBVH image then fits)
 #ifndef RTG_CAM_GRID
-#define RTG_CAM_GRID 0      // 1: the camera launch runs at most one one-wave block per 64 rays
-#endif
+#define RTG_CAM_GRID 1      // the camera launch runs at most one one-wave block per 64 rays (its one
+#endif                      // work counter then takes no probes from waves without work; +0.5 %)
 #ifndef RTG_POSTPONE
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
