@@ -76,6 +76,13 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
         // the payload and, on a hit, the triangle's shading record (issued before the tables' barrier)
         float4 ro = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f), rd = ro, h = ro;
         DevShade S;
+#if RTG_SHADE_EARLY
+        // (RTG_SHADE_EARLY) the throughput, the PCG state and the pixel index (for the PCG increment)
+        // are loaded before the barrier too, beside the shading record: no memory round trip after it
+        float4 e_thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+        uint64_t e_st = 0;
+        unsigned e_pix = 0;
+#endif
         if (valid) {
             unsigned j = i;  // bounce 0: the pixel's camera ray and first hit (k_generate), shared by its samples
             if (lean0) {
@@ -86,6 +93,15 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             rd = in_d[j];
             h = p.hits[j];
             if (h.x < RTG_FLT_MAX) S = s.shade[__float_as_int(h.y)];
+#if RTG_SHADE_EARLY
+            if (!lean0) {
+                e_thr = in_t[i];
+                e_st = in_r[i];
+            }
+            unsigned e_lp, e_sl;
+            split_pid(a, lean0 ? i : (unsigned)__float_as_int(ro.w), e_lp, e_sl);
+            e_pix = a.pixlist[e_lp];
+#endif
         }
         if (TAB) {
             // global_load_lds completes on vmcnt, not on the barrier: wait for it explicitly (the
@@ -97,13 +113,22 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
         if (valid) {
             pid = lean0 ? (int)i : __float_as_int(ro.w);  // the path id travels in ray_o.w
             const v3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
+#if RTG_SHADE_EARLY
+            const float4 thr4 = e_thr;
+#else
             const float4 thr4 = lean0 ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : in_t[i];
+#endif
             v3 thr = mk(thr4.x, thr4.y, thr4.z);
             const int can_hit = lean0 ? 1 : (rd.w != 0.0f);  // canHitLight travels in ray_d.w
             unsigned lp, sl;
             split_pid(a, (unsigned)pid, lp, sl);
+#if RTG_SHADE_EARLY
+            const uint64_t inc = pcg_inc(e_pix, a.s0 + sl);
+            uint64_t st = lean0 ? pcg_seed(a.seed, inc) : e_st;
+#else
             const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);  // (carrying it in the payload: slower)
             uint64_t st = lean0 ? pcg_seed(a.seed, inc) : in_r[i];
+#endif
             v3 c = mk(0.0f, 0.0f, 0.0f);
             int nterms = b + 1;
             // state carried past the environment lookup: a miss, or a path-traced hit (stage 1:

@@ -9,3 +9,5 @@ for m in none pg_first pg_after; do
   tail -1 $O/$m.log
   grep -h "k_accumulate_pm\|k_shade<false, true>\|k_trace<false, false>" $O/$m/kt_kernel_stats.csv | cut -d, -f1-4
 done
+cd $R
+AB_SETS="--steps 10;--config C2 --steps 20;--config C5 --spp 32 --steps 1;--config C4 --spp 64 --steps 1" bash tools/ab_leaf.sh 2>&1 | tee $O/ab_shade_early.txt
