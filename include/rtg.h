@@ -289,7 +289,8 @@ int  rtg_group_synchronize(rtg_group* g);
 int  rtg_group_film_read(rtg_group* g, float* rgb_sum /* width*height*3 */, uint32_t* spp);  /* reduces if needed */
 int  rtg_group_clear(rtg_group* g);
 double rtg_group_reduce_ms(rtg_group* g);  /* device time of the last reduce (set when the group is synchronized) */
-int  rtg_group_uses_rccl(rtg_group* g);    /* 1: RCCL communicator, 0: host-memory sum (repeated devices) */
+int  rtg_group_uses_rccl(rtg_group* g);    /* 1: RCCL communicator; 0: device copies (repeated devices) or one
+                                              device (no communicator unless RTG_GROUP_RCCL1=1 is set) */
 int  rtg_group_setup_ms(rtg_group* g, double* prepare_ms, double* upload_ms);  /* host build, parallel uploads */
 
 /* ---- own-tile film exchange (the data movement of rtg_group_reduce, exposed for hosts that run

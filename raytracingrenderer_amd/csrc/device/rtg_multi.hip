@@ -400,8 +400,10 @@ int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* de
                 g->h[r]->mem_cap = std::max<size_t>(1, freeb / 2 / (size_t)k);
         }
     }
-    // (A/B, round 6: RTG_GROUP_NO_RCCL1=1 forms no communicator for a group of one device)
-    if (g->distinct && (n_devices > 1 || !std::getenv("RTG_GROUP_NO_RCCL1"))) {
+    // A group of one device has nothing to exchange and forms no communicator: an RCCL communicator in
+    // the process slowed the renders by ~2 % (k_accumulate_pm 1.05 -> 1.52 ms per 64M-path fold,
+    // DESIGN.md §7). RTG_GROUP_RCCL1=1 forms one anyway (the tests of the RCCL setup on a 1-GPU box).
+    if (g->distinct && (n_devices > 1 || std::getenv("RTG_GROUP_RCCL1"))) {
         if (!load_rccl()) {
             rtg_group_destroy(g);
             return RTG_ERR_HIP;

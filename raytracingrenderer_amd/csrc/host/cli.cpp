@@ -88,7 +88,9 @@ int main(int argc, char** argv) {
             return die("rtg_group_create", rtg_last_error());
         if (rtg_group_set_options(grp, max_depth, RTG_OPT_CULL, 0) != 0) return die("rtg_group_set_options", rtg_last_error());
         std::printf("%d devices, own-tile film exchange by %s\n", (int)devices.size(),
-                    rtg_group_uses_rccl(grp) ? "RCCL (ncclSend/ncclRecv)" : "device copies (repeated devices)");
+                    rtg_group_uses_rccl(grp) ? "RCCL (ncclSend/ncclRecv)"
+                    : devices.size() == 1    ? "none (one device)"
+                                             : "device copies (repeated devices)");
     }
     std::printf("scene %s: %u triangles, %u lights, %dx%d (load %.0f ms, BVH %.0f ms)\n", scene_name.c_str(),
                 info.n_tris, info.n_lights, info.width, info.height, info.load_ms, info.bvh_ms);

@@ -285,18 +285,21 @@ def test_native_tile_partition_matches_python():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
-def test_group_film_equals_one_device(devices):
-    """rtg_group: one device through an RCCL communicator (ncclCommInitAll; one rank, so no
-    send/recv), or N ranks rehearsed on the box's one GPU (own tiles packed, moved by device copies,
-    scattered): the assembled film equals one handle's render of every tile, bit for bit."""
+@pytest.mark.parametrize("devices,rccl1", [([0], False), ([0], True), ([0, 0], False), ([0, 0, 0, 0, 0, 0, 0, 0], False)])
+def test_group_film_equals_one_device(devices, rccl1, monkeypatch):
+    """rtg_group: one device (no communicator; with RTG_GROUP_RCCL1=1 an RCCL communicator,
+    ncclCommInitAll, one rank, so no send/recv), or N ranks rehearsed on the box's one GPU (own tiles
+    packed, moved by device copies, scattered): the assembled film equals one handle's render of every
+    tile, bit for bit."""
     from raytracingrenderer_amd import RayTracer, RayTracerGroup, loadScene
+    if rccl1:
+        monkeypatch.setenv("RTG_GROUP_RCCL1", "1")
     s = loadScene(os.path.join(SCENES, "cornell-box"), width=200, height=136)
     one = RayTracer(s, seed=31)
     one.render(3, first_sample=0)
     want = one.film()[0]
     g = RayTracerGroup(s, devices=devices, seed=31)
-    assert g.uses_rccl == (len(set(devices)) == len(devices))
+    assert g.uses_rccl == rccl1
     g.render(2)
     g.render(1)
     got, spp = g.film()
@@ -358,7 +361,8 @@ def test_cli_multi_gpu_output_equals_single(tmp_path, opt):
     r2 = subprocess.run(base + opt, cwd=str(tmp_path / "multi"), capture_output=True, text=True, timeout=300)
     assert r1.returncode == 0, r1.stderr
     assert r2.returncode == 0, r2.stderr
-    assert ("RCCL" in r2.stdout) == (opt[0] == "-gpus")
+    assert ("by none (one device)" in r2.stdout) == (opt[0] == "-gpus")
+    assert ("device copies" in r2.stdout) == (opt[0] == "-devices")
     assert (tmp_path / "one" / "result_4.hdr").read_bytes() == (tmp_path / "multi" / "result_4.hdr").read_bytes()
 
 
