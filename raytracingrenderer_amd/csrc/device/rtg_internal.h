@@ -75,6 +75,9 @@ using namespace rtgd;
 #ifndef RTG_LDS_LIGHTS
 #define RTG_LDS_LIGHTS 48   // ... and the light table up to this many (80 B each): 5 x 48 < 256 threads
 #endif
+#ifndef RTG_SORT_OCT
+#define RTG_SORT_OCT 0      // 1: k_shade sorts each block's queue entries by ray direction octant
+#endif
 #ifndef RTG_SHADE_EARLY
 #define RTG_SHADE_EARLY 0   // 1: k_shade loads throughput, PCG state and pixel index before its barrier
 #endif

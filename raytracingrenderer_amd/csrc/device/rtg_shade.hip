@@ -24,6 +24,9 @@ template <bool ALT, bool TAB>
 __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
     __shared__ unsigned s_cnt[2][RTG_TB / 64];
     __shared__ unsigned s_base[2];
+#if RTG_SORT_OCT
+    __shared__ unsigned s_oct[2][RTG_TB / 64][8], s_off[2][RTG_TB / 64][8];
+#endif
     __shared__ float4 s_sho[RTG_TB], s_shd[RTG_TB];  // NEE ray staged until its queue position is known
     __shared__ DevMat s_mat[TAB ? RTG_LDS_MATS : 1];
     __shared__ DevLight s_lt[TAB ? RTG_LDS_LIGHTS : 1];
@@ -376,6 +379,57 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             p.meta[pid] = nterms;
         }
         // ---- block-level compaction of path ids into the next queues (one atomic per queue)
+#if RTG_SORT_OCT
+        // (RTG_SORT_OCT) each queue's rays of the block sorted by direction octant, so a traversal
+        // wave takes rays of one octant from neighbouring paths (queue order never changes a result)
+        {
+            const unsigned oe = ((n_d.x < 0.0f) ? 1u : 0u) | ((n_d.y < 0.0f) ? 2u : 0u) | ((n_d.z < 0.0f) ? 4u : 0u);
+            const float4 sdd = s_shd[threadIdx.x];
+            const unsigned os8 = ((sdd.x < 0.0f) ? 1u : 0u) | ((sdd.y < 0.0f) ? 2u : 0u) | ((sdd.z < 0.0f) ? 4u : 0u);
+            unsigned long long mine = 0, mins = 0;
+#pragma unroll
+            for (unsigned k = 0; k < 8; ++k) {
+                const unsigned long long be = __ballot(want_ext && oe == k);
+                const unsigned long long bs = __ballot(want_sh && os8 == k);
+                if (lane == 0) {
+                    s_oct[0][wave][k] = (unsigned)__popcll(be);
+                    s_oct[1][wave][k] = (unsigned)__popcll(bs);
+                }
+                if (oe == k) mine = be;
+                if (os8 == k) mins = bs;
+            }
+            __syncthreads();
+            if (threadIdx.x < 64) {
+                // off[q][w][k]: the block's rays of octant k before wave w's, after every lower octant
+                const unsigned q = threadIdx.x >> 5, w = (threadIdx.x >> 3) & 3u, k = threadIdx.x & 7u;
+                unsigned o = 0;
+                for (unsigned k2 = 0; k2 < k; ++k2)
+                    for (unsigned w2 = 0; w2 < RTG_TB / 64; ++w2) o += s_oct[q][w2][k2];
+                for (unsigned w2 = 0; w2 < w; ++w2) o += s_oct[q][w2][k];
+                s_off[q][w][k] = o;
+                if (w == 3 && k == 7) {
+                    const unsigned tot = o + s_oct[q][3][7];
+                    s_base[q] = tot ? atomicAdd(q == 0 ? &p.ctr[b + 1].ne8[32 * sg] : &p.ctr[b].ns8[32 * sg], tot) + sg * cap
+                                    : 0u;
+                }
+            }
+            __syncthreads();
+            if (want_ext) {
+                const unsigned j = s_base[0] + s_off[0][wave][oe] + prefix_lt(mine);
+                out_o[j] = n_o;
+                out_d[j] = n_d;
+                out_t[j] = n_t;
+                out_r[j] = n_r;
+            }
+            if (want_sh) {
+                const unsigned j = s_base[1] + s_off[1][wave][os8] + prefix_lt(mins);
+                p.shq[j] = (unsigned)pid;
+                p.sh_o[j] = s_sho[threadIdx.x];
+                p.sh_d[j] = sdd;
+            }
+            __syncthreads();
+        }
+#else
         const unsigned long long me = __ballot(want_ext);
         const unsigned long long ms = __ballot(want_sh);
         if (lane == 0) {
@@ -413,6 +467,7 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             p.sh_d[j] = s_shd[threadIdx.x];
         }
         __syncthreads();
+#endif
     }
 }
 
