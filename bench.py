@@ -40,8 +40,8 @@ L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth, same guide (§L2)
 # were taken on (the file's "spp", one GPU, the whole film)
 PMC_SUMMARIES = {c: os.path.join(ROOT, "profiles", "r06_pmc_traffic_%s.json" % c.lower()) for c in ("C2", "C3", "C4", "C5")}
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")  # round 5's C3 passes (fallback)
-KSTATS = os.path.join(ROOT, "profiles", "r05_kernel_stats.csv")       # rocprofv3 kernel-trace stats, same
-VALU_ISSUE = os.path.join(ROOT, "profiles", "r05_valu_issue.json")    # tools/valu_issue.py (SQ_INSTS_VALU passes)
+KSTATS = os.path.join(ROOT, "profiles", "r06_kernel_stats_c3.csv")   # rocprofv3 kernel-trace stats, same
+VALU_ISSUE = os.path.join(ROOT, "profiles", "r06_valu_issue.json")    # tools/valu_issue.py (SQ_INSTS_VALU passes)
 ROOF_SWEEP = os.path.join(ROOT, "profiles", "r02_roof_sweep.jsonl")  # tools/micro/roof.hip on an MI355X
 ROOF_REPLAY = os.path.join(ROOT, "profiles", "r05_roof_replay_c3.jsonl")  # tools/roof_replay.py (C3)
 # the replay ceiling of each workload (tools/replay_all.sh on an MI355X: tools/roof_replay.py at the
