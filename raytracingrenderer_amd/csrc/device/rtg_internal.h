@@ -43,15 +43,6 @@ using namespace rtgd;
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
 #endif
-#ifndef RTG_LEAF_MINWALK
-#define RTG_LEAF_MINWALK 0  // ... or once at most this many lanes can take a node step
-#endif
-#ifndef RTG_POP_PARK
-#define RTG_POP_PARK 0      // 1: a popped leaf is parked at once (one more pop) when no leaf is parked
-#endif
-#ifndef RTG_LEAF_SWAP
-#define RTG_LEAF_SWAP 0     // 1: a lane reaching a second leaf swaps it with its stack top and walks on
-#endif
 #ifndef RTG_REFILL
 #define RTG_REFILL 12       // refill idle lanes once at least this many are idle (the setup code then
                             // runs with more lanes per execution)
@@ -74,12 +65,6 @@ using namespace rtgd;
 #endif
 #ifndef RTG_LDS_LIGHTS
 #define RTG_LDS_LIGHTS 48   // ... and the light table up to this many (80 B each): 5 x 48 < 256 threads
-#endif
-#ifndef RTG_SORT_OCT
-#define RTG_SORT_OCT 0      // 1: k_shade sorts each block's queue entries by ray direction octant
-#endif
-#ifndef RTG_SHADE_EARLY
-#define RTG_SHADE_EARLY 0   // 1: k_shade loads throughput, PCG state and pixel index before its barrier
 #endif
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 7   // min waves per SIMD for k_shade (72 VGPRs, no spills; one tile per block)

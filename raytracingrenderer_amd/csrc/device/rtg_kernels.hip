@@ -403,15 +403,6 @@ void k_trace(SceneView s, TraceIO io) {
             pend = cur;
             cur = RTG_POP;
         }
-#if RTG_LEAF_SWAP
-        // a second leaf while one is parked: swap it with the stack's top entry (in LDS) and walk on;
-        // the leaf is popped again later (the order of the stack's subtrees does not change the result)
-        else if (cur < 0 && cur != RTG_EXIT && cur != RTG_POP && sp > 0 && sp <= STK) {
-            const int top = stk[sp - 1][tid];
-            stk[sp - 1][tid] = cur;
-            cur = top;
-        }
-#endif
         // ---- one pop for every branch: always an LDS read (ds_read, not a flat load through a
         // selected pointer); the global overflow read only for deep entries
         if (cur == RTG_POP) {
@@ -424,26 +415,11 @@ void k_trace(SceneView s, TraceIO io) {
                 if (COUNT && !anyr && sp < STK && kstk[sp][tid] > tbest) c_cullpop += 1;
                 if (sp >= STK) cur = io.ovf[(size_t)(sp - STK) * gthreads + gtid];
             }
-#if RTG_POP_PARK
-            // a popped leaf with no leaf parked: park it now and pop once more, so the lane has a
-            // node for the next iteration's step instead of spending that iteration parking
-            // (RTG_POP_PARK 2: the small-scene variant only)
-            if ((RTG_POP_PARK == 1 || SMALL) && cur < 0 && cur != RTG_EXIT && pend == RTG_EXIT) {
-                pend = cur;
-                if (sp == 0) {
-                    cur = RTG_EXIT;
-                } else {
-                    --sp;
-                    cur = stk[sp < STK ? sp : 0][tid];
-                    if (sp >= STK) cur = io.ovf[(size_t)(sp - STK) * gthreads + gtid];
-                }
-            }
-#endif
         }
         // leaf phase (wave-uniform): enough parked leaves, or no lane can walk on, or (the queue is
         // dry) any parked leaf: the drain is latency-bound, lanes should not wait for each other
         const unsigned long long pm = __ballot(pend != RTG_EXIT);
-        if (__popcll(pm) >= RTG_POSTPONE || __popcll(__ballot(cur >= 0)) <= RTG_LEAF_MINWALK || (drained && pm)) {
+        if (__popcll(pm) >= RTG_POSTPONE || __ballot(cur >= 0) == 0 || (drained && pm)) {
             if (COUNT) {
                 c_lslots += 64;
                 c_lstep += pend != RTG_EXIT ? 1 : 0;

@@ -24,9 +24,6 @@ template <bool ALT, bool TAB>
 __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, ChunkArgs a, PathBufs p, int b) {
     __shared__ unsigned s_cnt[2][RTG_TB / 64];
     __shared__ unsigned s_base[2];
-#if RTG_SORT_OCT
-    __shared__ unsigned s_oct[2][RTG_TB / 64][8], s_off[2][RTG_TB / 64][8];
-#endif
     __shared__ float4 s_sho[RTG_TB], s_shd[RTG_TB];  // NEE ray staged until its queue position is known
     __shared__ DevMat s_mat[TAB ? RTG_LDS_MATS : 1];
     __shared__ DevLight s_lt[TAB ? RTG_LDS_LIGHTS : 1];
@@ -79,13 +76,6 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
         // the payload and, on a hit, the triangle's shading record (issued before the tables' barrier)
         float4 ro = make_float4(a.cam.ox, a.cam.oy, a.cam.oz, 0.0f), rd = ro, h = ro;
         DevShade S;
-#if RTG_SHADE_EARLY
-        // (RTG_SHADE_EARLY) the throughput, the PCG state and the pixel index (for the PCG increment)
-        // are loaded before the barrier too, beside the shading record: no memory round trip after it
-        float4 e_thr = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
-        uint64_t e_st = 0;
-        unsigned e_pix = 0;
-#endif
         if (valid) {
             unsigned j = i;  // bounce 0: the pixel's camera ray and first hit (k_generate), shared by its samples
             if (lean0) {
@@ -96,15 +86,6 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             rd = in_d[j];
             h = p.hits[j];
             if (h.x < RTG_FLT_MAX) S = s.shade[__float_as_int(h.y)];
-#if RTG_SHADE_EARLY
-            if (!lean0) {
-                e_thr = in_t[i];
-                e_st = in_r[i];
-            }
-            unsigned e_lp, e_sl;
-            split_pid(a, lean0 ? i : (unsigned)__float_as_int(ro.w), e_lp, e_sl);
-            e_pix = a.pixlist[e_lp];
-#endif
         }
         if (TAB) {
             // global_load_lds completes on vmcnt, not on the barrier: wait for it explicitly (the
@@ -116,22 +97,13 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
         if (valid) {
             pid = lean0 ? (int)i : __float_as_int(ro.w);  // the path id travels in ray_o.w
             const v3 o = mk(ro.x, ro.y, ro.z), d = mk(rd.x, rd.y, rd.z);
-#if RTG_SHADE_EARLY
-            const float4 thr4 = e_thr;
-#else
             const float4 thr4 = lean0 ? make_float4(1.0f, 1.0f, 1.0f, 0.0f) : in_t[i];
-#endif
             v3 thr = mk(thr4.x, thr4.y, thr4.z);
             const int can_hit = lean0 ? 1 : (rd.w != 0.0f);  // canHitLight travels in ray_d.w
             unsigned lp, sl;
             split_pid(a, (unsigned)pid, lp, sl);
-#if RTG_SHADE_EARLY
-            const uint64_t inc = pcg_inc(e_pix, a.s0 + sl);
-            uint64_t st = lean0 ? pcg_seed(a.seed, inc) : e_st;
-#else
             const uint64_t inc = pcg_inc(a.pixlist[lp], a.s0 + sl);  // (carrying it in the payload: slower)
             uint64_t st = lean0 ? pcg_seed(a.seed, inc) : in_r[i];
-#endif
             v3 c = mk(0.0f, 0.0f, 0.0f);
             int nterms = b + 1;
             // state carried past the environment lookup: a miss, or a path-traced hit (stage 1:
@@ -379,57 +351,6 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             p.meta[pid] = nterms;
         }
         // ---- block-level compaction of path ids into the next queues (one atomic per queue)
-#if RTG_SORT_OCT
-        // (RTG_SORT_OCT) each queue's rays of the block sorted by direction octant, so a traversal
-        // wave takes rays of one octant from neighbouring paths (queue order never changes a result)
-        {
-            const unsigned oe = ((n_d.x < 0.0f) ? 1u : 0u) | ((n_d.y < 0.0f) ? 2u : 0u) | ((n_d.z < 0.0f) ? 4u : 0u);
-            const float4 sdd = s_shd[threadIdx.x];
-            const unsigned os8 = ((sdd.x < 0.0f) ? 1u : 0u) | ((sdd.y < 0.0f) ? 2u : 0u) | ((sdd.z < 0.0f) ? 4u : 0u);
-            unsigned long long mine = 0, mins = 0;
-#pragma unroll
-            for (unsigned k = 0; k < 8; ++k) {
-                const unsigned long long be = __ballot(want_ext && oe == k);
-                const unsigned long long bs = __ballot(want_sh && os8 == k);
-                if (lane == 0) {
-                    s_oct[0][wave][k] = (unsigned)__popcll(be);
-                    s_oct[1][wave][k] = (unsigned)__popcll(bs);
-                }
-                if (oe == k) mine = be;
-                if (os8 == k) mins = bs;
-            }
-            __syncthreads();
-            if (threadIdx.x < 64) {
-                // off[q][w][k]: the block's rays of octant k before wave w's, after every lower octant
-                const unsigned q = threadIdx.x >> 5, w = (threadIdx.x >> 3) & 3u, k = threadIdx.x & 7u;
-                unsigned o = 0;
-                for (unsigned k2 = 0; k2 < k; ++k2)
-                    for (unsigned w2 = 0; w2 < RTG_TB / 64; ++w2) o += s_oct[q][w2][k2];
-                for (unsigned w2 = 0; w2 < w; ++w2) o += s_oct[q][w2][k];
-                s_off[q][w][k] = o;
-                if (w == 3 && k == 7) {
-                    const unsigned tot = o + s_oct[q][3][7];
-                    s_base[q] = tot ? atomicAdd(q == 0 ? &p.ctr[b + 1].ne8[32 * sg] : &p.ctr[b].ns8[32 * sg], tot) + sg * cap
-                                    : 0u;
-                }
-            }
-            __syncthreads();
-            if (want_ext) {
-                const unsigned j = s_base[0] + s_off[0][wave][oe] + prefix_lt(mine);
-                out_o[j] = n_o;
-                out_d[j] = n_d;
-                out_t[j] = n_t;
-                out_r[j] = n_r;
-            }
-            if (want_sh) {
-                const unsigned j = s_base[1] + s_off[1][wave][os8] + prefix_lt(mins);
-                p.shq[j] = (unsigned)pid;
-                p.sh_o[j] = s_sho[threadIdx.x];
-                p.sh_d[j] = sdd;
-            }
-            __syncthreads();
-        }
-#else
         const unsigned long long me = __ballot(want_ext);
         const unsigned long long ms = __ballot(want_sh);
         if (lane == 0) {
@@ -467,7 +388,6 @@ __global__ __launch_bounds__(RTG_TB, RTG_SHADE_WAVES) void k_shade(SceneView s, 
             p.sh_d[j] = s_shd[threadIdx.x];
         }
         __syncthreads();
-#endif
     }
 }
 
