@@ -153,6 +153,9 @@ struct rtg_group {
     hipEvent_t xcopied = nullptr;              // repeated devices: devices[0] has copied every pack
     hipEvent_t xe0 = nullptr, xe1 = nullptr;   // devices[0]: rank 0's frames on its film / scatter done
     bool xtimed = false;                       // xe0 / xe1 hold an exchange not yet read into reduce_ms
+    // (test mode, RTG_GROUP_RCCL_SELF=1 with a communicator) rank 0 also sends its pack to itself
+    // with ncclSend / ncclRecv, so the RCCL exchange's calls run on a one-GPU box
+    bool rccl_self = false;
 };
 
 // the own-tile exchange's buffers: per rank its pixel list + pack buffer on its device, on devices[0]
@@ -181,7 +184,7 @@ static int exchange_setup(rtg_group* g) {
     for (size_t r = 0; r < n; ++r) {
         HIPOK(hipSetDevice(g->devices[r]));
         if (dev_upload(&g->d_pix[r], pl[r])) return RTG_ERR_HIP;
-        if (r == 0) g->d_pack[r] = g->d_recv;
+        if (r == 0 && !g->rccl_self) g->d_pack[r] = g->d_recv;
         else HIPOK(hipMalloc((void**)&g->d_pack[r], mp * 3 * sizeof(float)));
         HIPOK(hipStreamCreateWithFlags(&g->xs[r], hipStreamNonBlocking));
         HIPOK(hipEventCreateWithFlags(&g->xpacked[r], hipEventDisableTiming));
@@ -319,7 +322,7 @@ void rtg_group_destroy(rtg_group* g) {
     for (size_t r = 0; r < g->d_pix.size(); ++r) {
         (void)hipSetDevice(g->devices[r]);
         (void)hipFree(g->d_pix[r]);
-        if (r > 0) (void)hipFree(g->d_pack[r]);  // rank 0 packs straight into d_recv
+        if (r > 0 || g->rccl_self) (void)hipFree(g->d_pack[r]);  // rank 0 packs straight into d_recv
         if (r < g->xs.size() && g->xs[r]) (void)hipStreamDestroy(g->xs[r]);
         if (r < g->xpacked.size() && g->xpacked[r]) (void)hipEventDestroy(g->xpacked[r]);
     }
@@ -417,6 +420,7 @@ int rtg_group_create(const int* devices, int n_devices, const rtg_scene_desc* de
             return RTG_ERR_HIP;
         }
     }
+    g->rccl_self = !g->comms.empty() && std::getenv("RTG_GROUP_RCCL_SELF") != nullptr;
     if (hipSetDevice(g->devices[0]) != hipSuccess ||
         hipMalloc((void**)&g->d_sum, (size_t)g->W * g->H * 3 * sizeof(float)) != hipSuccess) {
         g_err = "rtg_group_create: film allocation failed";
@@ -496,7 +500,7 @@ int rtg_group_reduce_async(rtg_group* g) {
     if (int rc = rtg_film_gather(g->h[0], nullptr, 0, nullptr, g->xs[0])) return rc;
     HIPOK(hipSetDevice(g->devices[0]));
     HIPOK(hipEventRecord(g->xe0, g->xs[0]));
-    if (n == 1) {
+    if (n == 1 && !g->rccl_self) {
         // one device: its film is the film (one copy, not a pack and scatter of every pixel: C5's
         // 16.7M pixels took 0.97 ms that way); the handle's later folds wait for the copy
         HIPOK(hipMemcpyAsync(g->d_sum, g->h[0]->d_film, (size_t)film_pixels * 3 * sizeof(float), hipMemcpyDeviceToDevice,
@@ -518,7 +522,7 @@ int rtg_group_reduce_async(rtg_group* g) {
         // thread's RCCL group state stays balanced.
         if (g_rccl.group_start() != ncclSuccess) { g_err = "ncclGroupStart failed"; return RTG_ERR_HIP; }
         std::string fail;
-        for (size_t r = 1; r < n && fail.empty(); ++r) {
+        for (size_t r = g->rccl_self ? 0 : 1; r < n && fail.empty(); ++r) {
             if (!g->npix[r]) continue;
             const size_t cnt = (size_t)g->npix[r] * 3;
             ncclResult_t nr = g_rccl.send(g->d_pack[r], cnt, ncclFloat, 0, g->comms[r], g->xs[r]);

@@ -285,21 +285,25 @@ def test_native_tile_partition_matches_python():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices,rccl1", [([0], False), ([0], True), ([0, 0], False), ([0, 0, 0, 0, 0, 0, 0, 0], False)])
+@pytest.mark.parametrize("devices,rccl1", [([0], False), ([0], True), ([0], "self"), ([0, 0], False),
+                                           ([0, 0, 0, 0, 0, 0, 0, 0], False)])
 def test_group_film_equals_one_device(devices, rccl1, monkeypatch):
     """rtg_group: one device (no communicator; with RTG_GROUP_RCCL1=1 an RCCL communicator,
-    ncclCommInitAll, one rank, so no send/recv), or N ranks rehearsed on the box's one GPU (own tiles
-    packed, moved by device copies, scattered): the assembled film equals one handle's render of every
-    tile, bit for bit."""
+    ncclCommInitAll, one rank; with RTG_GROUP_RCCL_SELF=1 too, rank 0's pack goes through an
+    ncclSend / ncclRecv pair to itself, so the RCCL exchange's calls run on a one-GPU box), or N ranks
+    rehearsed on the box's one GPU (own tiles packed, moved by device copies, scattered): the
+    assembled film equals one handle's render of every tile, bit for bit."""
     from raytracingrenderer_amd import RayTracer, RayTracerGroup, loadScene
     if rccl1:
         monkeypatch.setenv("RTG_GROUP_RCCL1", "1")
+    if rccl1 == "self":
+        monkeypatch.setenv("RTG_GROUP_RCCL_SELF", "1")
     s = loadScene(os.path.join(SCENES, "cornell-box"), width=200, height=136)
     one = RayTracer(s, seed=31)
     one.render(3, first_sample=0)
     want = one.film()[0]
     g = RayTracerGroup(s, devices=devices, seed=31)
-    assert g.uses_rccl == rccl1
+    assert g.uses_rccl == bool(rccl1)
     g.render(2)
     g.render(1)
     got, spp = g.film()
@@ -311,13 +315,19 @@ def test_group_film_equals_one_device(devices, rccl1, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
-def test_queued_group_frames_equal_one_handle(devices):
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0, 0, 0, 0], "rccl_self"])
+def test_queued_group_frames_equal_one_handle(devices, monkeypatch):
     """The queued group frame (rtg_group_render_async + rtg_group_reduce_async, bench.py's lean step
     and the CLI's -gpus loop): four frames, each followed by a queued own-tile exchange with no host
     wait, then the film; and a film read between frames sees exactly the frames before it. Both equal
     one handle's waited-for renders of the same samples, bit for bit."""
     from raytracingrenderer_amd import RayTracer, RayTracerGroup, loadScene
+    if devices == "rccl_self":
+        # one device with a communicator, rank 0's pack sent to itself: the RCCL exchange's
+        # ncclSend / ncclRecv group, queued on the exchange stream, runs on a one-GPU box
+        monkeypatch.setenv("RTG_GROUP_RCCL1", "1")
+        monkeypatch.setenv("RTG_GROUP_RCCL_SELF", "1")
+        devices = [0]
     W, H = 160, 128  # 16 spp per frame: 328k paths, inside the frame pipeline's chunk limit
     s = loadScene(os.path.join(SCENES, "cornell-box"), width=W, height=H)
     ref = RayTracer(s, seed=23)
