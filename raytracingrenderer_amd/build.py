@@ -31,8 +31,11 @@ HOST_SRC = ["host/image_io.cpp", "host/jpeg_decode.cpp", "host/gem_json.cpp", "h
 DEVICE_SRC = ["device/rtg_kernels.hip", "device/rtg_shade.hip", "device/rtg_light.hip", "device/rtg_multi.hip",
               "device/rtg_bvh.hip"]
 # per-unit compile flags: k_shade's translation unit takes LLVM's max-ilp scheduler, which its
-# latency-bound body prefers, while the traversal keeps the default
-DEVICE_FLAGS = {"device/rtg_shade.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+# latency-bound body prefers, while the traversal keeps the default; the traversal's
+# unit is built without SLP vectorisation, whose packed FP32 pairs in the triangle test held k_trace at
+# 80 VGPRs (6 waves per SIMD); without them it needs 64 and runs at 7 (C3 +4 %)
+DEVICE_FLAGS = {"device/rtg_shade.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+                "device/rtg_kernels.hip": ["-fno-slp-vectorize"]}
 
 
 def _newer(out, deps):
@@ -139,7 +142,9 @@ def build_device(force=False, debug=False):
 
 def build_variant(name, extra_flags):
     """A/B variant of librtg (tools/mkab.sh): the product's units and flags plus `extra_flags`
-    (e.g. -DRTG_FOO=1), into lib/ab/<name>.so; loaded through RTG_LIB by tools/ab*.sh."""
+    (e.g. -DRTG_FOO=1), into lib/ab/<name>.so; loaded through RTG_LIB by tools/ab*.sh. A flag written
+    `unit:flag` (e.g. `rtg_kernels:-fslp-vectorize`) goes to that unit only; extra flags come after the
+    product's, so they override them."""
     d = os.path.join(LIB, "ab")
     os.makedirs(d, exist_ok=True)
     out = os.path.join(d, name + ".so")
@@ -148,8 +153,11 @@ def build_variant(name, extra_flags):
         objs, procs = [], []
         for rel, path in zip(DEVICE_SRC, src):
             obj = os.path.join(tmp, os.path.basename(rel) + ".o")
+            unit = os.path.splitext(os.path.basename(rel))[0]
+            flags = [f.split(":", 1)[1] if ":" in f else f for f in extra_flags
+                     if ":" not in f or f.split(":", 1)[0] == unit]
             cmd = ([HIPCC, "--offload-arch=" + ARCH] + DEVICE_CXXFLAGS + ['-DRTG_BUILD_ID="ab-%s"' % name] +
-                   list(extra_flags) + DEVICE_FLAGS.get(rel, []) + ["-c", "-o", obj, path])
+                   DEVICE_FLAGS.get(rel, []) + flags + ["-c", "-o", obj, path])
             procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
             objs.append(obj)
         for cmd, pr in procs:

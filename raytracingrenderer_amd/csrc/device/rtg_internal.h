@@ -24,8 +24,9 @@ using namespace rtgd;
 // Measured constants of the traversal and shading kernels (DESIGN.md §4 records the A/B runs;
 // the rejected alternatives are archived under tools/experiments/, not compiled in):
 #ifndef RTG_STACK
-#define RTG_STACK 24        // per-lane traversal stack entries kept in LDS (96 B per lane)
-#endif
+#define RTG_STACK 16        // per-lane traversal stack entries kept in LDS (64 B per lane; deeper entries
+#endif                      // go to the global overflow). 16 keeps a one-wave block at 4.1 KB of LDS for
+                            // 7 blocks per SIMD (20 entries: slower, 24: 6 per SIMD)
 // (the tuning constants are overridable with -D for A/B builds: tools/ab_matrix.sh)
 #ifndef RTG_STACK_SMALL
 #define RTG_STACK_SMALL 11  // the LDS stack of k_trace's small-scene variant (with its scene image in LDS)
@@ -48,8 +49,8 @@ using namespace rtgd;
                             // runs with more lanes per execution)
 #endif
 #ifndef RTG_TRACE_WPE
-#define RTG_TRACE_WPE 6     // minimum waves per SIMD requested for the traversal kernel (80 VGPRs)
-#endif
+#define RTG_TRACE_WPE 7     // minimum waves per SIMD requested for the traversal kernel: <= 72 VGPRs and
+#endif                      // <= 96 SGPRs (its unit is built without SLP vectorisation: 64 VGPRs, no spills)
 #define RTG_CULL_REL 1.52587890625e-05f  // 2^-16 relative inflation for distance culling
 #ifndef RTG_FETCH
 #define RTG_FETCH 256       // rays a wave takes from a work counter per atomic (k_trace pool)

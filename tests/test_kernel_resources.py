@@ -32,7 +32,8 @@ def kernels():
         for blk in md.split("  - .agpr_count")[1:]:
             name = re.search(r"\.name:\s+(\S+)", blk).group(1)
             res[name] = {k: int(re.search(r"\." + k + r":\s+(\d+)", blk).group(1))
-                         for k in ("vgpr_count", "vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size")}
+                         for k in ("vgpr_count", "vgpr_spill_count", "sgpr_count", "sgpr_spill_count",
+                                   "private_segment_fixed_size", "group_segment_fixed_size")}
     return res
 
 
@@ -42,12 +43,15 @@ def _find(kernels, prefix):
     return kernels[names[0]]
 
 
-def test_traversal_fits_six_waves_without_loop_spills(kernels):
-    k = _find(kernels, "_Z7k_traceILb0E")
-    assert k["vgpr_count"] <= 80  # 6 waves per SIMD
-    # two VGPRs of the stack-overflow pointer may live in scratch: they are read only when a lane's
-    # stack is deeper than its 24 LDS entries
-    assert k["vgpr_spill_count"] <= 2, k
+def test_traversal_fits_seven_waves_without_spills(kernels):
+    """k_trace (global-memory walk) at 7 waves per SIMD: VGPRs <= 72 (512 / 7, granule 8), SGPRs
+    <= 96 (800 / (ceil(n / 16) * 16 + 16) >= 7, MI355X_MICROARCH.md 'Residency'), no VGPR spills, and
+    a one-wave block's LDS (the 16-entry stack) small enough for 28 blocks per CU."""
+    k = _find(kernels, "_Z7k_traceILb0ELb0E")
+    assert k["vgpr_count"] <= 72, k
+    assert k["sgpr_count"] <= 96, k
+    assert k["vgpr_spill_count"] == 0 and k["private_segment_fixed_size"] == 0, k
+    assert 28 * k["group_segment_fixed_size"] <= 160 * 1024 and k["group_segment_fixed_size"] <= 4608, k
 
 
 def test_shading_kernel_does_not_spill(kernels):
