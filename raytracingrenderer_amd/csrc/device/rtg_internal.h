@@ -44,6 +44,9 @@ using namespace rtgd;
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
 #endif
+#ifndef RTG_PEND2
+#define RTG_PEND2 0         // A/B: a lane parks a second reached leaf instead of waiting for the leaf phase
+#endif
 #ifndef RTG_REFILL
 #define RTG_REFILL 12       // refill idle lanes once at least this many are idle (the setup code then
                             // runs with more lanes per execution)

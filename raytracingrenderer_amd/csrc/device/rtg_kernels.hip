@@ -109,6 +109,7 @@ void k_trace(SceneView s, TraceIO io) {
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tbest = 0.0f, omag = 0.0f, dmag = 0.0f, delta = 0.0f, bu = 0.0f, bv = 0.0f;
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0, pend = RTG_EXIT;
+    int pend2 = RTG_EXIT;  // RTG_PEND2: a second parked leaf
     bool occluded = false, wide = false, anyr = false;  // anyr: this lane's ray is a shadow ray
     const unsigned wslot = gtid >> 6;
     // RTG_DEBUG capture: the ray's record fetches in order (cap_k of them so far)
@@ -130,7 +131,7 @@ void k_trace(SceneView s, TraceIO io) {
     if (RTG_DEBUG && io.wtime && lane == 0) io.wtime[3 * wslot] = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         // ---- retire finished rays
-        if (have && cur == RTG_EXIT && pend == RTG_EXIT) {
+        if (have && cur == RTG_EXIT && pend == RTG_EXIT && (!RTG_PEND2 || pend2 == RTG_EXIT)) {
             if (anyr) {
                 if (io.visible) io.visible[pid] = occluded ? 0 : 1;
                 else if (bid == -2 ? occluded : !occluded)
@@ -204,6 +205,7 @@ void k_trace(SceneView s, TraceIO io) {
                     occluded = false;
                     sp = 0;
                     pend = RTG_EXIT;
+                    pend2 = RTG_EXIT;
                     // Wide walk only when every 1/d component is finite and nonzero (no NaN slab
                     // terms): then a passing descendant box implies its skipped ancestors pass.
                     // (|1/d| <= 2^64 and scene scale in [2^-60, 2^60] keep every product of the
@@ -224,11 +226,11 @@ void k_trace(SceneView s, TraceIO io) {
             c_nstep += (have && cur >= 0) ? 1 : 0;
             c_idle_e += !have ? 1 : 0;
             c_idle_ll += (have && cur == RTG_EXIT && pend != RTG_EXIT) ? 1 : 0;
-            c_idle_lb += (have && cur < 0 && cur != RTG_EXIT && pend != RTG_EXIT) ? 1 : 0;
+            c_idle_lb += (have && cur < 0 && cur != RTG_EXIT && pend != RTG_EXIT && (!RTG_PEND2 || pend2 != RTG_EXIT)) ? 1 : 0;
             c_idle_r += (have && cur == RTG_EXIT && pend == RTG_EXIT) ? 1 : 0;
             c_idle_lp += (have && cur < 0 && cur != RTG_EXIT && pend == RTG_EXIT) ? 1 : 0;
         }
-        if (!have || (cur == RTG_EXIT && pend == RTG_EXIT)) continue;
+        if (!have || (cur == RTG_EXIT && pend == RTG_EXIT && (!RTG_PEND2 || pend2 == RTG_EXIT))) continue;
         // Leaf: the reference's leaf loop (Geometry.h:420-431 / 446-458) over 1-2 triangles (a wide
         // leaf slot may join sibling reference leaves: up to RTG_LEAF_SPAN triangles).
         auto leaf = [&](const int word) {
@@ -402,6 +404,9 @@ void k_trace(SceneView s, TraceIO io) {
         if (cur < 0 && cur != RTG_EXIT && cur != RTG_POP && pend == RTG_EXIT) {
             pend = cur;
             cur = RTG_POP;
+        } else if (RTG_PEND2 && cur < 0 && cur != RTG_EXIT && cur != RTG_POP && pend2 == RTG_EXIT) {
+            pend2 = cur;
+            cur = RTG_POP;
         }
         // ---- one pop for every branch: always an LDS read (ds_read, not a flat load through a
         // selected pointer); the global overflow read only for deep entries
@@ -426,10 +431,12 @@ void k_trace(SceneView s, TraceIO io) {
             }
             if (pend != RTG_EXIT) {
                 leaf(pend);
-                pend = RTG_EXIT;
+                pend = RTG_PEND2 ? pend2 : RTG_EXIT;
+                if (RTG_PEND2) pend2 = RTG_EXIT;
                 if (anyr && occluded) {
                     cur = RTG_EXIT;
                     sp = 0;
+                    if (RTG_PEND2) pend = RTG_EXIT;
                 }
             }
         }
