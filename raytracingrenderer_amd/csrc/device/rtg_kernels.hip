@@ -109,7 +109,7 @@ void k_trace(SceneView s, TraceIO io) {
     v3 o = mk(0, 0, 0), d = mk(0, 0, 0), inv = mk(0, 0, 0);
     float tbest = 0.0f, omag = 0.0f, dmag = 0.0f, delta = 0.0f, bu = 0.0f, bv = 0.0f;
     int bid = -1, pid = 0, cur = RTG_EXIT, sp = 0, pend = RTG_EXIT;
-    int pend2 = RTG_EXIT;  // RTG_PEND2: a second parked leaf
+    int pend2 = RTG_EXIT;  // RTG_PEND2: a second parked leaf (the leaf phase runs pend, then pend2 moves up)
     bool occluded = false, wide = false, anyr = false;  // anyr: this lane's ray is a shadow ray
     const unsigned wslot = gtid >> 6;
     // RTG_DEBUG capture: the ray's record fetches in order (cap_k of them so far)
