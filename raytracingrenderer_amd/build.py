@@ -33,8 +33,9 @@ DEVICE_SRC = ["device/rtg_kernels.hip", "device/rtg_shade.hip", "device/rtg_ligh
 # per-unit compile flags: k_shade's translation unit takes LLVM's max-ilp scheduler, which its
 # latency-bound body prefers, while the traversal keeps the default; the traversal's
 # unit is built without SLP vectorisation, whose packed FP32 pairs in the triangle test held k_trace at
-# 80 VGPRs (6 waves per SIMD); without them it needs 64 and runs at 7 (C3 +4 %)
-DEVICE_FLAGS = {"device/rtg_shade.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+# 80 VGPRs (6 waves per SIMD); without them it needs 64 and runs at 7 (C3 +4 %). k_shade
+# without it too: 62 instead of 68 VGPRs, fewer pair moves (C5 shading -4 %)
+DEVICE_FLAGS = {"device/rtg_shade.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp", "-fno-slp-vectorize"],
                 "device/rtg_kernels.hip": ["-fno-slp-vectorize"]}
 
 

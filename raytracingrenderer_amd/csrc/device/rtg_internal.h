@@ -29,11 +29,12 @@ using namespace rtgd;
                             // 7 blocks per SIMD (20 entries: slower, 24: 6 per SIMD)
 // (the tuning constants are overridable with -D for A/B builds: tools/ab_matrix.sh)
 #ifndef RTG_STACK_SMALL
-#define RTG_STACK_SMALL 11  // the LDS stack of k_trace's small-scene variant (with its scene image in LDS)
+#define RTG_STACK_SMALL 7   // the LDS stack of k_trace's small-scene variant (with its scene image in LDS)
 #endif
 #ifndef RTG_SMALL_F4
-#define RTG_SMALL_F4 224    // small-scene image limit, float4s (3.5 KB): 11 x 256 B of stack + 3.5 KB per
-#endif                      // one-wave block keeps 24 blocks per CU in the 160 KB of LDS
+#define RTG_SMALL_F4 192    // small-scene image limit, float4s (3 KB; cornell's SBVH image is 188): with
+#endif                      // 7 x 256 B of stack a one-wave block takes 4.9 KB, 28 blocks (7 waves) per CU
+                            // (224 float4s and 11 entries: 6.5 KB, 6 waves; C2 walk -7 %)
 #ifndef RTG_SMALL_LB
 #define RTG_SMALL_LB 0      // 1: the small-scene image holds the leaf boxes too; 0: they stay in global
 #endif                      // memory, read once per candidate hit (C2 +4.8 %: cornell's SBVH image then fits)

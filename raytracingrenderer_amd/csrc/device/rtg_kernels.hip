@@ -59,7 +59,8 @@ static __device__ __forceinline__ void trace_slice(const TraceIO& io, unsigned n
 
 // SMALL: the scene's wide nodes, triangle records and leaf boxes are copied into LDS at the start of
 // each block (SceneView::img, small scenes only) and the walk reads them there; the LDS stack is then
-// RTG_STACK_SMALL entries, so the block's LDS stays what a 24-entry stack takes.
+// RTG_STACK_SMALL entries, so the block's LDS stays below 5 KB (7 one-wave blocks per SIMD, as the
+// global walk's 16-entry stack).
 template <bool COUNT, bool SMALL>
 __global__ __launch_bounds__(RTG_TTB) __attribute__((amdgpu_waves_per_eu(RTG_TRACE_WPE)))
 void k_trace(SceneView s, TraceIO io) {

@@ -52,6 +52,10 @@ def test_traversal_fits_seven_waves_without_spills(kernels):
     assert k["sgpr_count"] <= 96, k
     assert k["vgpr_spill_count"] == 0 and k["private_segment_fixed_size"] == 0, k
     assert 28 * k["group_segment_fixed_size"] <= 160 * 1024 and k["group_segment_fixed_size"] <= 4608, k
+    # the small-scene variant (scene image + 7-entry stack in LDS) at the same 7 blocks per SIMD
+    ks = _find(kernels, "_Z7k_traceILb0ELb1E")
+    assert ks["vgpr_count"] <= 72 and ks["sgpr_count"] <= 96 and ks["vgpr_spill_count"] == 0, ks
+    assert ks["group_segment_fixed_size"] <= 5120, ks
 
 
 def test_shading_kernel_does_not_spill(kernels):
