@@ -135,7 +135,7 @@ typedef struct rtg_stats {
     /* summed like node_lane_steps (lane_slots = node_lane_steps + these five)                      */
     uint64_t lane_idle_no_ray;       /* no ray: waiting for the wave's refill                        */
     uint64_t lane_idle_last_leaf;    /* walk done, its parked leaf waiting for the wave's leaf phase */
-    uint64_t lane_idle_leaf_blocked; /* reached a second leaf while one is parked                    */
+    uint64_t lane_idle_leaf_blocked; /* reached a leaf while its parked-leaf slots are full (two)    */
     uint64_t lane_idle_retiring;     /* ray finished, retired at the next iteration                  */
     uint64_t lane_idle_leaf_popped;  /* popped a leaf last iteration; parked in this one             */
 } rtg_stats;

@@ -79,7 +79,7 @@ void k_trace(SceneView s, TraceIO io) {
                        c_cullpop = 0, c_pops = 0, c_lslots = 0, c_lbox = 0;
     unsigned c_tails = 0;  // triangle records whose last 16 B were fetched (COUNT)
     // COUNT: why a lane is not stepping a node in an iteration: no ray, its walk done but its parked
-    // leaf not run yet, a second leaf reached while one is parked, retiring this iteration, a leaf
+    // leaf not run yet, a leaf reached while both parked-leaf slots are full, retiring this iteration, a leaf
     // popped last iteration (parked in this one)
     unsigned long long c_idle_e = 0, c_idle_ll = 0, c_idle_lb = 0, c_idle_r = 0, c_idle_lp = 0;
     unsigned pool_base = 0, pool_left = 0, last_b = 0;  // wave-uniform

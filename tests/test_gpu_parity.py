@@ -486,16 +486,18 @@ def test_cli_matches_library(tmp_path):
     assert read_hdr(str(tmp_path / "result_3.hdr")).shape == (64, 64, 3)
 
 
-@pytest.mark.parametrize("base", [2.0, 4.0])
-def test_deep_bvh_stack_overflow(tmp_path, base):
-    """Triangles at x = base^k make a chain-like BVH (depth 17 / 30): rays along +x keep one sibling
-    per level pending, past the 24-entry LDS stack, into the global overflow. base 2 keeps the
-    scene scale under 2^60 (compressed wide walk); base 4 exceeds it (exact BVH2 walk)."""
+@pytest.mark.parametrize("base,n_tris", [(2.0, 60), (4.0, 60), (2.0, 28)])
+def test_deep_bvh_stack_overflow(tmp_path, base, n_tris):
+    """Triangles at x = base^k make a chain-like BVH (depth 17 / 26 with 60 triangles): rays along +x
+    keep one sibling per level pending, past the 16-entry LDS stack, into the global overflow. base 2
+    keeps the scene scale under 2^60 (compressed wide walk); base 4 exceeds it (exact BVH2 walk). 28
+    triangles are a small scene by construction (at most 27 wide nodes: 4 * 27 + 3 * 28 <= 192 float4s),
+    walked from LDS with a 7-entry stack."""
     from raytracingrenderer_amd.renderer import write_mesh_scene
-    P = np.array([[(base ** k, -1.0, -1.0), (base ** k, 1.0, -1.0), (base ** k, 0.0, 1.0)] for k in range(60)],
+    P = np.array([[(base ** k, -1.0, -1.0), (base ** k, 1.0, -1.0), (base ** k, 0.0, 1.0)] for k in range(n_tris)],
                  np.float32)
     s = loadScene(write_mesh_scene(str(tmp_path), P, 32, 32))
-    assert s.info.bvh_depth >= 17
+    assert s.info.bvh_depth >= (17 if n_tris == 60 else 9)
     rng = np.random.default_rng(3)
     n = 4096
     r = np.zeros((n, 8), np.float32)
