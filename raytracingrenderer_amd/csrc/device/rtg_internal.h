@@ -45,6 +45,10 @@ using namespace rtgd;
 #define RTG_POSTPONE 32     // park a reached leaf and keep walking; run the leaves of a wave together
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
 #endif
+#ifndef RTG_MEM_PCT
+#define RTG_MEM_PCT 60      // percent of the free HBM the path state of the chunks in flight may take (50:
+                            // C5 runs its 32 spp as two 16-spp chunks, -3 %)
+#endif
 #ifndef RTG_PEND2
 #define RTG_PEND2 1         // a lane parks a second reached leaf instead of idling until the leaf phase
 #endif                      // (node-step lane use 0.70 -> 0.77 on C3: +1 to +2 %)

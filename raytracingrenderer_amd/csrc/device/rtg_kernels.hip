@@ -1777,13 +1777,13 @@ int render_impl(rtg_handle* h, uint32_t first, uint32_t n_samples, uint64_t seed
     // events work across the slots' streams: overlapped launches then count their shared time twice)
     const bool diag = h->serial || (RTG_DEBUG && (h->wavetime || h->capture_launch >= 0));
     {
-        // path state of the chunks in flight takes at most half the free HBM (buffers held now count
-        // as free); pipelined chunks keep RTG_SLOTS sets
+        // path state of the chunks in flight takes at most RTG_MEM_PCT % of the free HBM (buffers held
+        // now count as free); pipelined chunks keep RTG_SLOTS sets
         size_t freeb = 0, totalb = 0;
         if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
             size_t held = 0;
             for (const ChunkSlot& sl : h->slot) held += slot_bytes(sl);
-            size_t budget = (freeb + held) / 2;
+            size_t budget = (freeb + held) / 100 * RTG_MEM_PCT;
             if (h->mem_cap) budget = std::min(budget, h->mem_cap);
             const size_t per_pix = path_bytes(planes, false) * std::max<size_t>(1, h->npix);
             size_t max_ns = budget / per_pix;
