@@ -46,8 +46,9 @@ using namespace rtgd;
                             // once this many lanes hold one (or no lane can walk on, or the queue is dry)
 #endif
 #ifndef RTG_MEM_PCT
-#define RTG_MEM_PCT 60      // percent of the free HBM the path state of the chunks in flight may take (50:
-                            // C5 runs its 32 spp as two 16-spp chunks, -3 %)
+#define RTG_MEM_PCT 50      // percent of the free HBM the path state of the chunks in flight may take (60:
+                            // C5's 32-spp step in one chunk, +3 % once allocated, but allocations past
+                            // ~half the VRAM take seconds: a one-shot C5 frame 4.8 -> 8.4 s)
 #endif
 #ifndef RTG_PEND2
 #define RTG_PEND2 1         // a lane parks a second reached leaf instead of idling until the leaf phase
