@@ -229,7 +229,7 @@ void k_trace(SceneView s, TraceIO io) {
             c_idle_ll += (have && cur == RTG_EXIT && pend != RTG_EXIT) ? 1 : 0;
             c_idle_lb += (have && cur < 0 && cur != RTG_EXIT && pend != RTG_EXIT && (!RTG_PEND2 || pend2 != RTG_EXIT)) ? 1 : 0;
             c_idle_r += (have && cur == RTG_EXIT && pend == RTG_EXIT) ? 1 : 0;
-            c_idle_lp += (have && cur < 0 && cur != RTG_EXIT && pend == RTG_EXIT) ? 1 : 0;
+            c_idle_lp += (have && cur < 0 && cur != RTG_EXIT && (pend == RTG_EXIT || (RTG_PEND2 && pend2 == RTG_EXIT))) ? 1 : 0;
         }
         if (!have || (cur == RTG_EXIT && pend == RTG_EXIT && (!RTG_PEND2 || pend2 == RTG_EXIT))) continue;
         // Leaf: the reference's leaf loop (Geometry.h:420-431 / 446-458) over 1-2 triangles (a wide

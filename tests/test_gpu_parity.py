@@ -808,6 +808,10 @@ def test_count_mode_counters_are_consistent(synth20k, cornell256):
         tris = s["tri_tests"] + s["shadow_tri_tests"]
         assert 0 < s["leafbox_tests"] <= s["tri_tail_loads"] <= tris, s
         assert s["node_lane_steps"] > 0 and s["extension_rays"] > 0, s
+        # every lane of every loop iteration is stepping a node or idle for exactly one reason (the
+        # bench's lane_idle_node shares; two parked-leaf slots: a lane with a free slot parks its leaf)
+        idle = sum(s["lane_idle_" + k] for k in ("no_ray", "last_leaf", "leaf_blocked", "retiring", "leaf_popped"))
+        assert s["lane_slots"] == s["node_lane_steps"] + idle, s
 
 
 @pytest.mark.host_glibc
